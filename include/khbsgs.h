@@ -1,0 +1,114 @@
+/*
+ * khbsgs.h — C ABI of the MI355X (gfx950) BSGS giant-step library, libkhbsgs.so.
+ *
+ * This is the drop-in boundary for keyhunt's GPU path.  It replaces the reference's unwired
+ * CUDA surface (cuda/bsgs_kernel.cu:230-319: cudaInit, cudaAllocateBSGSMemory,
+ * cudaCopyToDevice, cudaLaunchBSGS, cudaCopyFromDevice, cudaFreeMemory) and takes over exactly
+ * the CPU work of keyhunt.cpp:3867-4004 — the per-(chunk, target) giant-step group loop of
+ * thread_process_bsgs with its level-1 bloom probe.  Candidates it returns feed the host's
+ * bsgs_secondcheck (keyhunt.cpp:3948 -> 4271-4368), unchanged.
+ *
+ * Conventions
+ *   - Every function returns 0 (KHB_OK) or a negative KHB_E* code; khb_strerror() names it.
+ *     The library never prints.
+ *   - One context per device; a context is used by one host thread at a time.  Distinct
+ *     contexts are independent (thread-safe across devices).
+ *   - 256-bit field elements and points cross the boundary big-endian: a point is x||y, 64 bytes,
+ *     each coordinate Int::Get32Bytes order (secp256k1/Int.cpp:308-316).
+ *   - The caller keeps ownership of every host buffer; tables are copied into device memory.
+ *   - Missing or non-gfx950 GPU: khb_open fails with KHB_ENODEV.  There is no CPU fallback.
+ */
+#ifndef KHBSGS_H
+#define KHBSGS_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KHB_OK 0
+#define KHB_EINVAL -1     /* bad argument / shape */
+#define KHB_ENODEV -2     /* no usable gfx950 device */
+#define KHB_ENOMEM -3     /* device or pinned allocation failed */
+#define KHB_EHIP -4       /* HIP runtime error (khb_last_hip_error() has the hipError_t) */
+#define KHB_ESTATE -5     /* call order violated (e.g. scan before tables are loaded) */
+#define KHB_EBUSY -6      /* a submission is still in flight */
+
+#define KHB_GROUP 1024         /* giant steps per group: CPU_GRP_SIZE, keyhunt.cpp:127 */
+#define KHB_GIANT_TABLE 513    /* GSn[0..511] + _2GSn, keyhunt.cpp:1318-1338 */
+
+typedef struct khb_ctx khb_ctx;
+
+/* One level-1 bloom hit: giant step `a` (= group*1024 + t, keyhunt.cpp:3948) of job `job`. */
+typedef struct {
+  uint32_t job;
+  uint32_t a;
+} khb_cand;
+
+/* A group whose batch inverse collapsed (some dx == 0: the target sits exactly on a window
+ * centre, SURVEY.md §8a quirk ii).  Reported so the host can mirror the reference. */
+typedef struct {
+  uint32_t job;
+  uint32_t group;
+} khb_degenerate;
+
+typedef struct {
+  uint32_t n_cand;         /* total hits (may exceed the capacity given to khb_collect) */
+  uint32_t n_degenerate;
+  uint64_t giant_steps;    /* giant steps scanned by the submission */
+  float kernel_ms;         /* device time of the scan kernel (HIP events on the ctx stream) */
+} khb_stats;
+
+/* ---- device / context ---- */
+int khb_device_count(int* n);
+/* lanes: persistent-grid size in work lanes (0 = auto: 8 waves per CU).  Sizes the scratch. */
+int khb_open(int device, uint32_t lanes, khb_ctx** out);
+int khb_close(khb_ctx* ctx);
+const char* khb_strerror(int code);
+int khb_last_hip_error(const khb_ctx* ctx);
+/* The hipStream_t the context launches on (for external HIP events / synchronisation). */
+void* khb_stream(khb_ctx* ctx);
+
+/* ---- tables (bsgs setup, keyhunt.cpp:1185-1364) ---- */
+/* Level-1 bloom: 256 sub-blooms of identical geometry concatenated in sub-bloom order
+ * (bloom_bP[0..255].bf, bloom.h:26-45).  bits/hashes as in struct bloom. */
+int khb_load_bloom(khb_ctx* ctx, const uint8_t* bf_concat, uint64_t bytes_per_sub, uint64_t bits_per_sub,
+                   uint32_t hashes);
+/* GSn[0..511] and _2GSn (keyhunt.cpp:1325-1338), 513 affine points x||y BE. */
+int khb_load_giant_table(khb_ctx* ctx, const uint8_t* gsn_xy_be);
+/* Lane start offsets: offs[m] = (m*groups_per_lane) * _2GSn, m in [0, n) (offs[0] unused: the
+ * identity).  A lane owns groups [m*groups_per_lane, (m+1)*groups_per_lane) of a job. */
+int khb_load_lane_offsets(khb_ctx* ctx, const uint8_t* offs_xy_be, uint32_t n, uint32_t groups_per_lane);
+
+/* ---- scan ---- */
+/* Enqueue the group loop for n_jobs jobs.  centres[k] (x||y BE) is startP of job k, i.e.
+ * target + (order - base - (2M*512 + M))*G (keyhunt.cpp:3861-3869), the centre of group 0.
+ * Every job scans groups [group_begin, group_begin + group_count); group_begin must be a
+ * multiple of groups_per_lane.  Returns immediately (stream-ordered). */
+int khb_submit(khb_ctx* ctx, const uint8_t* centres_xy_be, uint32_t n_jobs, uint32_t group_begin,
+               uint32_t group_count);
+/* Wait for the last submission; copy up to cap candidates (unordered) and degenerate-group
+ * records.  stats may be NULL. */
+int khb_collect(khb_ctx* ctx, khb_cand* cand, uint32_t cap, khb_degenerate* degen, uint32_t degen_cap,
+                khb_stats* stats);
+/* Convenience: submit + collect. */
+int khb_scan(khb_ctx* ctx, const uint8_t* centres_xy_be, uint32_t n_jobs, uint32_t group_begin,
+             uint32_t group_count, khb_cand* cand, uint32_t cap, khb_stats* stats);
+
+/* ---- parity / debug ---- */
+/* x-coordinates (BE, probe order t = 0..1023 per group) of groups [group_begin,
+ * group_begin+group_count) of ONE job; xs must hold group_count*1024*32 bytes. */
+int khb_dump_x(khb_ctx* ctx, const uint8_t* centre_xy_be, uint32_t group_begin, uint32_t group_count,
+               uint8_t* xs);
+/* Field self-test kernel: r[i] = op(a[i], b[i]) for op 0=mul 1=sqr 2=add 3=sub 4=inv;
+ * 32-byte BE values. */
+int khb_field_op(khb_ctx* ctx, int op, const uint8_t* a, const uint8_t* b, uint8_t* r, uint32_t n);
+/* Bloom self-test kernel: hit[i] = bloom_check(level-1, x[i]) for 32-byte BE x values. */
+int khb_probe(khb_ctx* ctx, const uint8_t* xs, uint8_t* hit, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

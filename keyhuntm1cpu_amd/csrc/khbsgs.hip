@@ -1,0 +1,543 @@
+// libkhbsgs.so — MI355X (gfx950) BSGS giant-step engine behind the C ABI of include/khbsgs.h.
+//
+// Hot path replaced: keyhunt.cpp:3867-4004 (thread_process_bsgs group loop + level-1 bloom probe).
+//
+// Work decomposition:
+//   job   = one (chunk, target) pair; the host supplies its group-0 centre startP.
+//   lane  = one work item = `groups_per_lane` consecutive 1024-point groups of one job.  The lane
+//           derives its first centre as startP + offs[m] (one affine add), then walks its groups
+//           exactly as the reference walks a chunk: per group a 513-element Montgomery batch
+//           inverse (prefix products spilled to a lane-private HBM scratch, coalesced across the
+//           wave), 1023 x-only affine additions, 1024 bloom probes, and the next-centre add.
+//   grid  = persistent: `lanes` work lanes stride over n_jobs * lanes_per_job items.
+// One lane's group maps 1:1 onto one reference group, so a collapsed batch inverse (dx == 0)
+// reproduces the reference's all-zero inverses exactly (IntGroup.cpp:36-58 + IntMod.cpp:497-500).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdlib.h>
+#include <new>
+#include "../../include/khbsgs.h"
+#include "device/fe.hpp"
+#include "device/bloom_probe.hpp"
+
+using namespace khb;
+
+namespace {
+
+struct AffPt {
+  Fe x, y;
+};
+
+constexpr uint32_t kBlock = 256;
+constexpr uint32_t kHalf = KHB_GROUP / 2;            // 512
+constexpr uint32_t kCandCap = 1u << 20;
+constexpr uint32_t kDegenCap = 4096;
+
+struct ScanArgs {
+  const uint8_t* __restrict__ bloom;
+  BloomGeom geom;
+  const AffPt* __restrict__ gsn;       // [0..511] GSn, [512] _2GSn
+  const AffPt* __restrict__ offs;      // lane start offsets
+  const AffPt* __restrict__ centres;   // per-job group-0 centre
+  Fe* __restrict__ scratch;            // prefix products [512][lanes]
+  khb_cand* __restrict__ cand;
+  khb_degenerate* __restrict__ degen;
+  uint32_t* __restrict__ counters;     // [0] candidates [1] degenerate groups
+  uint8_t* __restrict__ xdump;         // DUMP builds only
+  uint64_t n_items;
+  uint32_t n_jobs, group_begin, group_end, gpl, lanes_per_job, stride, cand_cap, degen_cap;
+};
+
+__device__ __forceinline__ void emit_cand(const ScanArgs& A, uint32_t job, uint32_t a) {
+  uint32_t k = atomicAdd(&A.counters[0], 1u);
+  if (k < A.cand_cap) A.cand[k] = khb_cand{job, a};
+}
+
+template <bool DUMP>
+__device__ __forceinline__ void probe(const ScanArgs& A, const Fe& x, uint32_t job, uint32_t j, uint32_t t) {
+  if (DUMP) {
+    uint8_t* o = A.xdump + ((uint64_t)(j - A.group_begin) * KHB_GROUP + t) * 32;
+    fe_to_be(o, x);
+  } else {
+    if (bloom_probe_x(A.bloom, A.geom, x)) emit_cand(A, job, j * KHB_GROUP + t);
+  }
+}
+
+// One reference group (keyhunt.cpp:3873-3999) centred on C; advances C to the next centre.
+template <bool DUMP>
+__device__ __forceinline__ void scan_group(const ScanArgs& A, AffPt& C, uint32_t job, uint32_t j, Fe* scr) {
+  const uint32_t S = A.stride;
+  const AffPt* __restrict__ gsn = A.gsn;
+  Fe acc, dx;
+  // forward pass: prefix products of dx[i] = GSn[i].x - C.x (i < 512) and _2GSn.x - C.x
+  fe_sub(acc, gsn[0].x, C.x);
+  scr[0] = acc;
+  for (uint32_t i = 1; i < kHalf; ++i) {
+    fe_sub(dx, gsn[i].x, C.x);
+    fe_mul(acc, acc, dx);
+    scr[(size_t)i * S] = acc;
+  }
+  fe_sub(dx, gsn[kHalf].x, C.x);
+  fe_mul(acc, acc, dx);
+  const bool degenerate = fe_is_zero(acc);
+  Fe inv;
+  fe_inv(inv, acc);                       // 0 when degenerate -> every inverse 0, as the reference
+  // i = 512: inverse of _2GSn.x - C.x, kept for the next centre
+  Fe inv2, pre;
+  pre = scr[(size_t)(kHalf - 1) * S];
+  fe_mul(inv2, inv, pre);
+  fe_mul(inv, inv, dx);
+  for (int i = (int)kHalf - 1; i >= 0; --i) {
+    Fe idx;
+    if (i > 0) {
+      pre = scr[(size_t)(i - 1) * S];
+      fe_mul(idx, inv, pre);
+      fe_sub(dx, gsn[i].x, C.x);
+      fe_mul(inv, inv, dx);
+    } else {
+      idx = inv;
+    }
+    Fe u, s, x;
+    fe_add(u, C.x, gsn[i].x);             // x = s^2 - C.x - GSn.x
+    // C - GSn[i]: s = (-GSn.y - C.y)/dx; only s^2 is needed
+    fe_add(s, gsn[i].y, C.y);
+    fe_mul(s, s, idx);
+    fe_sqr(x, s);
+    fe_sub(x, x, u);
+    probe<DUMP>(A, x, job, j, kHalf - 1 - (uint32_t)i);
+    if (i < (int)kHalf - 1) {
+      // C + GSn[i]: s = (GSn.y - C.y)/dx
+      fe_sub(s, gsn[i].y, C.y);
+      fe_mul(s, s, idx);
+      fe_sqr(x, s);
+      fe_sub(x, x, u);
+      probe<DUMP>(A, x, job, j, kHalf + 1 + (uint32_t)i);
+    }
+  }
+  probe<DUMP>(A, C.x, job, j, kHalf);
+  // next centre: C + _2GSn with y (keyhunt.cpp:3986-3999)
+  {
+    const AffPt& g2 = gsn[kHalf];
+    Fe s, nx, ny;
+    fe_sub(s, g2.y, C.y);
+    fe_mul(s, s, inv2);
+    fe_sqr(nx, s);
+    fe_sub(nx, nx, C.x);
+    fe_sub(nx, nx, g2.x);
+    fe_sub(ny, g2.x, nx);
+    fe_mul(ny, ny, s);
+    fe_sub(ny, ny, g2.y);
+    C.x = nx;
+    C.y = ny;
+  }
+  if (!DUMP && degenerate) {
+    uint32_t k = atomicAdd(&A.counters[1], 1u);
+    if (k < A.degen_cap) A.degen[k] = khb_degenerate{job, j};
+  }
+}
+
+// AddDirect (SECP256K1.cpp:242-265) with its own inversion; used once per lane.
+__device__ __forceinline__ bool add_direct(AffPt& r, const AffPt& p1, const AffPt& p2) {
+  Fe dy, dx, s, x, y;
+  fe_sub(dy, p2.y, p1.y);
+  fe_sub(dx, p2.x, p1.x);
+  const bool degenerate = fe_is_zero(dx);
+  fe_inv(dx, dx);
+  fe_mul(s, dy, dx);
+  fe_sqr(x, s);
+  fe_sub(x, x, p1.x);
+  fe_sub(x, x, p2.x);
+  fe_sub(y, p2.x, x);
+  fe_mul(y, y, s);
+  fe_sub(y, y, p2.y);
+  r.x = x;
+  r.y = y;
+  return degenerate;
+}
+
+template <bool DUMP>
+__global__ __launch_bounds__(kBlock, 2) void k_giant_scan(ScanArgs A) {
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+  Fe* scr = A.scratch + lane;
+  for (uint64_t item = lane; item < A.n_items; item += A.stride) {
+    const uint32_t job = (uint32_t)(item / A.lanes_per_job);
+    const uint32_t m = (uint32_t)(item % A.lanes_per_job);
+    const uint32_t g0 = A.group_begin + m * A.gpl;
+    const uint32_t g1 = min(g0 + A.gpl, A.group_end);
+    AffPt C = A.centres[job];
+    const uint32_t mo = g0 / A.gpl;
+    if (mo != 0) {
+      if (add_direct(C, C, A.offs[mo]) && !DUMP) {
+        uint32_t k = atomicAdd(&A.counters[1], 1u);
+        if (k < A.degen_cap) A.degen[k] = khb_degenerate{job, g0 | 0x80000000u};
+      }
+    }
+    for (uint32_t j = g0; j < g1; ++j) scan_group<DUMP>(A, C, job, j, scr);
+  }
+}
+
+__global__ void k_field_op(int op, const Fe* __restrict__ a, const Fe* __restrict__ b, Fe* __restrict__ r, uint32_t n) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fe x = a[i], y = b[i], z;
+  switch (op) {
+    case 0: fe_mul(z, x, y); break;
+    case 1: fe_sqr(z, x); break;
+    case 2: fe_add(z, x, y); break;
+    case 3: fe_sub(z, x, y); break;
+    default: fe_inv(z, x); break;
+  }
+  r[i] = z;
+}
+
+__global__ void k_probe(const uint8_t* __restrict__ bloom, BloomGeom g, const Fe* __restrict__ xs, uint8_t* hit, uint32_t n) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  hit[i] = bloom_probe_x(bloom, g, xs[i]) ? 1 : 0;
+}
+
+}  // namespace
+
+struct khb_ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  int last_hip = 0;
+  uint32_t lanes = 0;
+  uint8_t* d_bloom = nullptr;
+  BloomGeom geom{};
+  AffPt* d_gsn = nullptr;
+  AffPt* d_offs = nullptr;
+  uint32_t n_offs = 0, gpl = 0;
+  AffPt* d_centres = nullptr;
+  uint32_t centres_cap = 0;
+  Fe* d_scratch = nullptr;
+  khb_cand* d_cand = nullptr;
+  khb_degenerate* d_degen = nullptr;
+  uint32_t* d_counters = nullptr;
+  uint32_t* h_counters = nullptr;      // pinned
+  AffPt* h_centres = nullptr;          // pinned staging
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool in_flight = false;
+  uint64_t pending_steps = 0;
+};
+
+namespace {
+
+int hip_fail(khb_ctx* c, hipError_t e) {
+  if (c) c->last_hip = (int)e;
+  return e == hipErrorOutOfMemory ? KHB_ENOMEM : KHB_EHIP;
+}
+#define KHB_TRY(c, x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return hip_fail((c), e_); } while (0)
+
+void pts_from_be(AffPt* dst, const uint8_t* src, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) {
+    fe_from_be(dst[i].x, src + 64 * (size_t)i);
+    fe_from_be(dst[i].y, src + 64 * (size_t)i + 32);
+  }
+}
+
+int ensure_centres(khb_ctx* c, uint32_t n) {
+  if (n <= c->centres_cap) return KHB_OK;
+  if (c->d_centres) hipFree(c->d_centres);
+  if (c->h_centres) hipHostFree(c->h_centres);
+  c->d_centres = nullptr;
+  c->h_centres = nullptr;
+  c->centres_cap = 0;
+  uint32_t cap = n < 1024 ? 1024 : n;
+  KHB_TRY(c, hipMalloc(&c->d_centres, sizeof(AffPt) * cap));
+  KHB_TRY(c, hipHostMalloc((void**)&c->h_centres, sizeof(AffPt) * cap, hipHostMallocDefault));
+  c->centres_cap = cap;
+  return KHB_OK;
+}
+
+ScanArgs make_args(khb_ctx* c, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count) {
+  ScanArgs A{};
+  A.bloom = c->d_bloom;
+  A.geom = c->geom;
+  A.gsn = c->d_gsn;
+  A.offs = c->d_offs;
+  A.centres = c->d_centres;
+  A.scratch = c->d_scratch;
+  A.cand = c->d_cand;
+  A.degen = c->d_degen;
+  A.counters = c->d_counters;
+  A.n_jobs = n_jobs;
+  A.group_begin = group_begin;
+  A.group_end = group_begin + group_count;
+  A.gpl = c->gpl;
+  A.lanes_per_job = (group_count + c->gpl - 1) / c->gpl;
+  A.n_items = (uint64_t)n_jobs * A.lanes_per_job;
+  A.stride = c->lanes;
+  A.cand_cap = kCandCap;
+  A.degen_cap = kDegenCap;
+  return A;
+}
+
+int check_scan_args(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count) {
+  if (!c || !centres || n_jobs == 0 || group_count == 0) return KHB_EINVAL;
+  if (!c->d_gsn || !c->d_offs || c->gpl == 0) return KHB_ESTATE;
+  if (group_begin % c->gpl) return KHB_EINVAL;
+  uint64_t end = (uint64_t)group_begin + group_count;
+  if (end * KHB_GROUP > 0xFFFFFFFFull) return KHB_EINVAL;         // a = j*1024+t fits 32 bits (keyhunt.cpp:3948)
+  if ((end + c->gpl - 1) / c->gpl > c->n_offs) return KHB_EINVAL;  // offsets table too short
+  return KHB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* khb_strerror(int code) {
+  switch (code) {
+    case KHB_OK: return "ok";
+    case KHB_EINVAL: return "invalid argument";
+    case KHB_ENODEV: return "no usable gfx950 device";
+    case KHB_ENOMEM: return "out of memory";
+    case KHB_EHIP: return "HIP runtime error";
+    case KHB_ESTATE: return "call order violated (tables not loaded?)";
+    case KHB_EBUSY: return "submission in flight";
+    default: return "unknown error";
+  }
+}
+
+int khb_last_hip_error(const khb_ctx* c) { return c ? c->last_hip : 0; }
+void* khb_stream(khb_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int khb_device_count(int* n) {
+  if (!n) return KHB_EINVAL;
+  int k = 0;
+  if (hipGetDeviceCount(&k) != hipSuccess) k = 0;
+  *n = k;
+  return KHB_OK;
+}
+
+int khb_open(int device, uint32_t lanes, khb_ctx** out) {
+  if (!out) return KHB_EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return KHB_ENODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return KHB_ENODEV;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return KHB_ENODEV;
+  khb_ctx* c = new (std::nothrow) khb_ctx();
+  if (!c) return KHB_ENOMEM;
+  c->device = device;
+  if (lanes == 0) lanes = (uint32_t)prop.multiProcessorCount * 8u * 64u;
+  lanes = (lanes + kBlock - 1) / kBlock * kBlock;
+  c->lanes = lanes;
+  int rc = KHB_OK;
+  auto fail = [&](hipError_t e) { rc = hip_fail(c, e); khb_close(c); return rc; };
+  hipError_t e;
+  if ((e = hipSetDevice(device)) != hipSuccess) return fail(e);
+  if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&c->d_scratch, sizeof(Fe) * (size_t)kHalf * lanes)) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&c->d_cand, sizeof(khb_cand) * kCandCap)) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&c->d_degen, sizeof(khb_degenerate) * kDegenCap)) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&c->d_counters, 16)) != hipSuccess) return fail(e);
+  if ((e = hipHostMalloc((void**)&c->h_counters, 16, hipHostMallocDefault)) != hipSuccess) return fail(e);
+  if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return fail(e);
+  if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return fail(e);
+  *out = c;
+  return KHB_OK;
+}
+
+int khb_close(khb_ctx* c) {
+  if (!c) return KHB_OK;
+  if (c->device >= 0) hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  hipFree(c->d_bloom);
+  hipFree(c->d_gsn);
+  hipFree(c->d_offs);
+  hipFree(c->d_centres);
+  hipFree(c->d_scratch);
+  hipFree(c->d_cand);
+  hipFree(c->d_degen);
+  hipFree(c->d_counters);
+  if (c->h_counters) hipHostFree(c->h_counters);
+  if (c->h_centres) hipHostFree(c->h_centres);
+  if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+  return KHB_OK;
+}
+
+int khb_load_bloom(khb_ctx* c, const uint8_t* bf, uint64_t bytes_per_sub, uint64_t bits_per_sub, uint32_t hashes) {
+  if (!c || !bf || bytes_per_sub == 0 || bits_per_sub < 2 || hashes == 0 || hashes > 255) return KHB_EINVAL;
+  if ((bits_per_sub + 7) / 8 != bytes_per_sub) return KHB_EINVAL;    // bloom.cpp:110-113
+  if (c->in_flight) return KHB_EBUSY;
+  KHB_TRY(c, hipSetDevice(c->device));
+  if (c->d_bloom) { hipFree(c->d_bloom); c->d_bloom = nullptr; }
+  const size_t total = (size_t)bytes_per_sub * 256;
+  KHB_TRY(c, hipMalloc(&c->d_bloom, total));
+  KHB_TRY(c, hipMemcpy(c->d_bloom, bf, total, hipMemcpyHostToDevice));
+  c->geom.bytes_per_sub = bytes_per_sub;
+  c->geom.bits = bits_per_sub;
+  c->geom.magic = (uint64_t)(((unsigned __int128)1 << 64) / bits_per_sub);
+  c->geom.wrap = (uint64_t)(((unsigned __int128)1 << 64) % bits_per_sub);
+  c->geom.hashes = hashes;
+  return KHB_OK;
+}
+
+int khb_load_giant_table(khb_ctx* c, const uint8_t* gsn) {
+  if (!c || !gsn) return KHB_EINVAL;
+  if (c->in_flight) return KHB_EBUSY;
+  KHB_TRY(c, hipSetDevice(c->device));
+  AffPt h[KHB_GIANT_TABLE];
+  pts_from_be(h, gsn, KHB_GIANT_TABLE);
+  if (!c->d_gsn) KHB_TRY(c, hipMalloc(&c->d_gsn, sizeof(h)));
+  KHB_TRY(c, hipMemcpy(c->d_gsn, h, sizeof(h), hipMemcpyHostToDevice));
+  return KHB_OK;
+}
+
+int khb_load_lane_offsets(khb_ctx* c, const uint8_t* offs, uint32_t n, uint32_t gpl) {
+  if (!c || !offs || n == 0 || gpl == 0) return KHB_EINVAL;
+  if (c->in_flight) return KHB_EBUSY;
+  KHB_TRY(c, hipSetDevice(c->device));
+  AffPt* h = (AffPt*)malloc(sizeof(AffPt) * n);
+  if (!h) return KHB_ENOMEM;
+  pts_from_be(h, offs, n);
+  if (c->d_offs) { hipFree(c->d_offs); c->d_offs = nullptr; }
+  hipError_t e = hipMalloc(&c->d_offs, sizeof(AffPt) * n);
+  if (e == hipSuccess) e = hipMemcpy(c->d_offs, h, sizeof(AffPt) * n, hipMemcpyHostToDevice);
+  free(h);
+  if (e != hipSuccess) return hip_fail(c, e);
+  c->n_offs = n;
+  c->gpl = gpl;
+  return KHB_OK;
+}
+
+int khb_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count) {
+  int rc = check_scan_args(c, centres, n_jobs, group_begin, group_count);
+  if (rc) return rc;
+  if (!c->d_bloom) return KHB_ESTATE;
+  if (c->in_flight) return KHB_EBUSY;
+  KHB_TRY(c, hipSetDevice(c->device));
+  if ((rc = ensure_centres(c, n_jobs))) return rc;
+  pts_from_be(c->h_centres, centres, n_jobs);
+  KHB_TRY(c, hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, c->stream));
+  KHB_TRY(c, hipMemsetAsync(c->d_counters, 0, 16, c->stream));
+  ScanArgs A = make_args(c, n_jobs, group_begin, group_count);
+  const uint32_t blocks = c->lanes / kBlock;
+  KHB_TRY(c, hipEventRecord(c->ev0, c->stream));
+  hipLaunchKernelGGL(k_giant_scan<false>, dim3(blocks), dim3(kBlock), 0, c->stream, A);
+  KHB_TRY(c, hipGetLastError());
+  KHB_TRY(c, hipEventRecord(c->ev1, c->stream));
+  KHB_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, 16, hipMemcpyDeviceToHost, c->stream));
+  c->in_flight = true;
+  c->pending_steps = (uint64_t)n_jobs * group_count * KHB_GROUP;
+  return KHB_OK;
+}
+
+int khb_collect(khb_ctx* c, khb_cand* cand, uint32_t cap, khb_degenerate* degen, uint32_t degen_cap, khb_stats* st) {
+  if (!c) return KHB_EINVAL;
+  if (!c->in_flight) return KHB_ESTATE;
+  KHB_TRY(c, hipSetDevice(c->device));
+  c->in_flight = false;
+  KHB_TRY(c, hipStreamSynchronize(c->stream));
+  const uint32_t nc = c->h_counters[0], nd = c->h_counters[1];
+  uint32_t take = nc < kCandCap ? nc : kCandCap;
+  if (take > cap) take = cap;
+  if (take && cand) KHB_TRY(c, hipMemcpy(cand, c->d_cand, sizeof(khb_cand) * take, hipMemcpyDeviceToHost));
+  uint32_t dt = nd < kDegenCap ? nd : kDegenCap;
+  if (dt > degen_cap) dt = degen_cap;
+  if (dt && degen) KHB_TRY(c, hipMemcpy(degen, c->d_degen, sizeof(khb_degenerate) * dt, hipMemcpyDeviceToHost));
+  if (st) {
+    st->n_cand = nc;
+    st->n_degenerate = nd;
+    st->giant_steps = c->pending_steps;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) ms = -1.f;
+    st->kernel_ms = ms;
+  }
+  return KHB_OK;
+}
+
+int khb_scan(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count,
+             khb_cand* cand, uint32_t cap, khb_stats* st) {
+  int rc = khb_submit(c, centres, n_jobs, group_begin, group_count);
+  if (rc) return rc;
+  return khb_collect(c, cand, cap, nullptr, 0, st);
+}
+
+int khb_dump_x(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint32_t group_count, uint8_t* xs) {
+  int rc = check_scan_args(c, centre, 1, group_begin, group_count);
+  if (rc) return rc;
+  if (!xs) return KHB_EINVAL;
+  if (c->in_flight) return KHB_EBUSY;
+  KHB_TRY(c, hipSetDevice(c->device));
+  if ((rc = ensure_centres(c, 1))) return rc;
+  pts_from_be(c->h_centres, centre, 1);
+  const size_t bytes = (size_t)group_count * KHB_GROUP * 32;
+  uint8_t* d_x = nullptr;
+  KHB_TRY(c, hipMalloc(&d_x, bytes));
+  hipError_t e = hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, 16, c->stream);
+  if (e == hipSuccess) {
+    ScanArgs A = make_args(c, 1, group_begin, group_count);
+    A.xdump = d_x;
+    const uint32_t blocks = (uint32_t)((A.n_items + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_giant_scan<true>, dim3(blocks < c->lanes / kBlock ? blocks : c->lanes / kBlock),
+                       dim3(kBlock), 0, c->stream, A);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipMemcpy(xs, d_x, bytes, hipMemcpyDeviceToHost);
+  hipFree(d_x);
+  if (e != hipSuccess) return hip_fail(c, e);
+  return KHB_OK;
+}
+
+int khb_field_op(khb_ctx* c, int op, const uint8_t* a, const uint8_t* b, uint8_t* r, uint32_t n) {
+  if (!c || !a || !r || n == 0 || op < 0 || op > 4 || (op != 1 && op != 4 && !b)) return KHB_EINVAL;
+  KHB_TRY(c, hipSetDevice(c->device));
+  Fe* h = (Fe*)malloc(sizeof(Fe) * n * 3);
+  if (!h) return KHB_ENOMEM;
+  for (uint32_t i = 0; i < n; ++i) {
+    fe_from_be(h[i], a + 32 * (size_t)i);
+    if (b) fe_from_be(h[n + i], b + 32 * (size_t)i); else h[n + i] = Fe{};
+  }
+  Fe* d = nullptr;
+  hipError_t e = hipMalloc(&d, sizeof(Fe) * n * 3);
+  if (e == hipSuccess) e = hipMemcpy(d, h, sizeof(Fe) * n * 2, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_field_op, dim3((n + 255) / 256), dim3(256), 0, c->stream, op, d, d + n, d + 2 * n, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipMemcpy(h + 2 * n, d + 2 * n, sizeof(Fe) * n, hipMemcpyDeviceToHost);
+  if (e == hipSuccess)
+    for (uint32_t i = 0; i < n; ++i) fe_to_be(r + 32 * (size_t)i, h[2 * n + i]);
+  hipFree(d);
+  free(h);
+  if (e != hipSuccess) return hip_fail(c, e);
+  return KHB_OK;
+}
+
+int khb_probe(khb_ctx* c, const uint8_t* xs, uint8_t* hit, uint32_t n) {
+  if (!c || !xs || !hit || n == 0) return KHB_EINVAL;
+  if (!c->d_bloom) return KHB_ESTATE;
+  KHB_TRY(c, hipSetDevice(c->device));
+  Fe* h = (Fe*)malloc(sizeof(Fe) * n);
+  if (!h) return KHB_ENOMEM;
+  for (uint32_t i = 0; i < n; ++i) fe_from_be(h[i], xs + 32 * (size_t)i);
+  Fe* d = nullptr;
+  uint8_t* dh = nullptr;
+  hipError_t e = hipMalloc(&d, sizeof(Fe) * n);
+  if (e == hipSuccess) e = hipMalloc(&dh, n);
+  if (e == hipSuccess) e = hipMemcpy(d, h, sizeof(Fe) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_probe, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->d_bloom, c->geom, d, dh, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipMemcpy(hit, dh, n, hipMemcpyDeviceToHost);
+  hipFree(d);
+  hipFree(dh);
+  free(h);
+  if (e != hipSuccess) return hip_fail(c, e);
+  return KHB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,147 @@
+"""ctypes binding of libkhbsgs.so (include/khbsgs.h): the MI355X giant-step scan.
+
+Replaces the CPU group loop of keyhunt.cpp:3867-4004 (thread_process_bsgs).  No fallback: if the
+library or a gfx950 device is missing, KhbError is raised.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import LIB_DIR
+
+LIB_PATH = os.path.join(LIB_DIR, "libkhbsgs.so")
+
+KHB_GROUP = 1024
+
+
+class KhbError(RuntimeError):
+    pass
+
+
+class Cand(C.Structure):
+    _fields_ = [("job", C.c_uint32), ("a", C.c_uint32)]
+
+
+class Degenerate(C.Structure):
+    _fields_ = [("job", C.c_uint32), ("group", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("n_cand", C.c_uint32), ("n_degenerate", C.c_uint32), ("giant_steps", C.c_uint64),
+                ("kernel_ms", C.c_float)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise KhbError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        P = C.POINTER
+        L.khb_device_count.argtypes = [P(C.c_int)]
+        L.khb_open.argtypes = [C.c_int, C.c_uint32, P(C.c_void_p)]
+        L.khb_close.argtypes = [C.c_void_p]
+        L.khb_strerror.restype = C.c_char_p
+        L.khb_strerror.argtypes = [C.c_int]
+        L.khb_last_hip_error.argtypes = [C.c_void_p]
+        L.khb_stream.restype = C.c_void_p
+        L.khb_stream.argtypes = [C.c_void_p]
+        L.khb_load_bloom.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, C.c_uint64, C.c_uint32]
+        L.khb_load_giant_table.argtypes = [C.c_void_p, C.c_char_p]
+        L.khb_load_lane_offsets.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32]
+        L.khb_submit.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]
+        L.khb_collect.argtypes = [C.c_void_p, P(Cand), C.c_uint32, P(Degenerate), C.c_uint32, P(Stats)]
+        L.khb_scan.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32, P(Cand), C.c_uint32,
+                               P(Stats)]
+        L.khb_dump_x.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_char_p]
+        L.khb_field_op.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint32]
+        L.khb_probe.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_uint32]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, ctx=None) -> None:
+    if rc != 0:
+        msg = lib().khb_strerror(rc).decode()
+        if ctx:
+            msg += f" (hipError {lib().khb_last_hip_error(ctx)})"
+        raise KhbError(f"khbsgs: {msg} [{rc}]")
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    _check(lib().khb_device_count(C.byref(n)))
+    return n.value
+
+
+class Engine:
+    """One libkhbsgs context (one device)."""
+
+    def __init__(self, device: int = 0, lanes: int = 0):
+        self.h = C.c_void_p()
+        _check(lib().khb_open(device, lanes, C.byref(self.h)))
+        self.gpl = 0
+
+    def close(self) -> None:
+        if self.h:
+            lib().khb_close(self.h)
+            self.h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def stream(self) -> int:
+        return int(lib().khb_stream(self.h) or 0)
+
+    def load_bloom(self, bf: bytes, bytes_per_sub: int, bits: int, hashes: int) -> None:
+        assert len(bf) == 256 * bytes_per_sub
+        _check(lib().khb_load_bloom(self.h, bf, bytes_per_sub, bits, hashes), self.h)
+
+    def load_giant_table(self, gsn: bytes) -> None:
+        assert len(gsn) == 513 * 64
+        _check(lib().khb_load_giant_table(self.h, gsn), self.h)
+
+    def load_lane_offsets(self, offs: bytes, gpl: int) -> None:
+        assert len(offs) % 64 == 0
+        _check(lib().khb_load_lane_offsets(self.h, offs, len(offs) // 64, gpl), self.h)
+        self.gpl = gpl
+
+    def submit(self, centres: bytes, group_begin: int, group_count: int) -> None:
+        _check(lib().khb_submit(self.h, centres, len(centres) // 64, group_begin, group_count), self.h)
+
+    def collect(self, cap: int = 1 << 20):
+        cand = (Cand * cap)()
+        deg = (Degenerate * 4096)()
+        st = Stats()
+        _check(lib().khb_collect(self.h, cand, cap, deg, 4096, C.byref(st)), self.h)
+        n = min(st.n_cand, cap)
+        return ([(int(cand[i].job), int(cand[i].a)) for i in range(n)],
+                [(int(deg[i].job), int(deg[i].group)) for i in range(min(st.n_degenerate, 4096))], st)
+
+    def scan(self, centres: bytes, group_begin: int, group_count: int, cap: int = 1 << 20):
+        self.submit(centres, group_begin, group_count)
+        return self.collect(cap)
+
+    def dump_x(self, centre: bytes, group_begin: int, group_count: int) -> bytes:
+        out = C.create_string_buffer(group_count * KHB_GROUP * 32)
+        _check(lib().khb_dump_x(self.h, centre, group_begin, group_count, out), self.h)
+        return out.raw
+
+    def field_op(self, op: int, a: bytes, b: bytes | None) -> bytes:
+        n = len(a) // 32
+        out = C.create_string_buffer(n * 32)
+        _check(lib().khb_field_op(self.h, op, a, b, out, n), self.h)
+        return out.raw
+
+    def probe(self, xs: bytes) -> bytes:
+        n = len(xs) // 32
+        out = C.create_string_buffer(n)
+        _check(lib().khb_probe(self.h, xs, out, n), self.h)
+        return out.raw

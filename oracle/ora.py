@@ -1,0 +1,234 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of oracle/build/liboracle.so (the plain-C restatement of the reference BSGS path,
+see ora.h).  Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg —
+never by the product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+
+
+class U256(C.Structure):
+    _fields_ = [("w", C.c_uint64 * 4)]
+
+    @classmethod
+    def of(cls, v: int) -> "U256":
+        u = cls()
+        for i in range(4):
+            u.w[i] = (v >> (64 * i)) & 0xFFFFFFFFFFFFFFFF
+        return u
+
+    def value(self) -> int:
+        return sum(int(self.w[i]) << (64 * i) for i in range(4))
+
+
+class Point(C.Structure):
+    _fields_ = [("x", U256), ("y", U256), ("z", U256)]
+
+    def xy(self) -> tuple[int, int]:
+        return self.x.value(), self.y.value()
+
+    def be64(self) -> bytes:
+        return self.x.value().to_bytes(32, "big") + self.y.value().to_bytes(32, "big")
+
+    @classmethod
+    def of(cls, x: int, y: int) -> "Point":
+        p = cls()
+        p.x = U256.of(x)
+        p.y = U256.of(y)
+        p.z = U256.of(1)
+        return p
+
+
+class Bloom(C.Structure):
+    _fields_ = [("entries", C.c_uint64), ("bits", C.c_uint64), ("bytes", C.c_uint64), ("hashes", C.c_uint8),
+                ("error", C.c_longdouble), ("ready", C.c_uint8), ("major", C.c_uint8), ("minor", C.c_uint8),
+                ("bpe", C.c_double), ("bf", C.POINTER(C.c_uint8))]
+
+
+class XValue(C.Structure):
+    _fields_ = [("value", C.c_uint8 * 6), ("pad", C.c_uint8 * 2), ("index", C.c_uint64)]
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P = C.POINTER
+        L.ora_xxh64.restype = C.c_uint64
+        L.ora_xxh64.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
+        L.ora_bsgs_new.restype = C.c_void_p
+        L.ora_bsgs_new.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_char_p, C.c_size_t]
+        L.ora_bsgs_free.argtypes = [C.c_void_p]
+        L.ora_bsgs_params.argtypes = [C.c_void_p, P(C.c_uint64)]
+        L.ora_bsgs_bloom.restype = P(Bloom)
+        L.ora_bsgs_bloom.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.ora_bsgs_bptable.restype = P(XValue)
+        L.ora_bsgs_bptable.argtypes = [C.c_void_p]
+        L.ora_bsgs_giant_table.argtypes = [C.c_void_p, C.c_char_p]
+        L.ora_bsgs_amp_table.argtypes = [C.c_void_p, C.c_int, C.c_char_p]
+        L.ora_bsgs_chunk_start.argtypes = [C.c_void_p, P(U256), P(Point), P(Point)]
+        L.ora_bsgs_scan.argtypes = [C.c_void_p, P(Point), C.c_uint32, C.c_uint32, C.c_void_p, P(C.c_uint64),
+                                    C.c_uint32, P(C.c_uint32), P(Point)]
+        L.ora_bsgs_secondcheck.restype = C.c_int
+        L.ora_bsgs_secondcheck.argtypes = [C.c_void_p, P(U256), C.c_uint32, P(Point), P(U256)]
+        L.ora_bsgs_search.restype = C.c_uint64
+        L.ora_bsgs_search.argtypes = [C.c_void_p, P(Point), C.c_int, P(U256), P(U256), C.c_uint64, P(C.c_int),
+                                      P(U256)]
+        L.ora_bsgs_bench.restype = C.c_uint64
+        L.ora_bsgs_bench.argtypes = [C.c_void_p, P(Point), P(U256), C.c_int, C.c_double, P(C.c_double)]
+        L.ora_compute_pubkey.argtypes = [P(Point), P(U256)]
+        L.ora_add_direct.argtypes = [P(Point), P(Point), P(Point)]
+        L.ora_negation.argtypes = [P(Point), P(Point)]
+        L.ora_parse_pubkey_hex.restype = C.c_int
+        L.ora_parse_pubkey_hex.argtypes = [C.c_char_p, P(Point), P(C.c_int)]
+        L.ora_pubkey_hex.argtypes = [P(Point), C.c_int, C.c_char_p]
+        L.ora_bloom_init2.restype = C.c_int
+        L.ora_bloom_init2.argtypes = [P(Bloom), C.c_uint64, C.c_longdouble]
+        L.ora_bloom_free.argtypes = [P(Bloom)]
+        L.ora_bloom_add.restype = C.c_int
+        L.ora_bloom_add.argtypes = [P(Bloom), C.c_void_p, C.c_int]
+        L.ora_bloom_check.restype = C.c_int
+        L.ora_bloom_check.argtypes = [P(Bloom), C.c_void_p, C.c_int]
+        _lib = L
+    return _lib
+
+
+def xxh64(data: bytes, seed: int) -> int:
+    return int(lib().ora_xxh64(data, len(data), seed))
+
+
+def pubkey(k: int) -> Point:
+    p = Point()
+    lib().ora_compute_pubkey(C.byref(p), C.byref(U256.of(k)))
+    return p
+
+
+def pubkey_hex(k: int, compressed: bool = True) -> str:
+    buf = C.create_string_buffer(140)
+    lib().ora_pubkey_hex(C.byref(pubkey(k)), 1 if compressed else 0, buf)
+    return buf.value.decode()
+
+
+def parse_pubkey(s: str) -> tuple[Point, bool] | None:
+    p = Point()
+    comp = C.c_int(0)
+    if not lib().ora_parse_pubkey_hex(s.encode(), C.byref(p), C.byref(comp)):
+        return None
+    return p, bool(comp.value)
+
+
+def add_direct(a: Point, b: Point) -> Point:
+    r = Point()
+    lib().ora_add_direct(C.byref(r), C.byref(a), C.byref(b))
+    return r
+
+
+def negation(a: Point) -> Point:
+    r = Point()
+    lib().ora_negation(C.byref(r), C.byref(a))
+    return r
+
+
+class Bsgs:
+    """The reference BSGS geometry + tables (keyhunt.cpp:1045-1880) built by the oracle."""
+
+    def __init__(self, n: str | None = None, k: int = 1, threads: int = 8):
+        err = C.create_string_buffer(256)
+        self.h = lib().ora_bsgs_new(n.encode() if n else None, k, threads, err, 256)
+        if not self.h:
+            raise ValueError(err.value.decode())
+        p = (C.c_uint64 * 10)()
+        lib().ora_bsgs_params(self.h, p)
+        (self.m, self.m2, self.m3, self.aux, self.cycles, self.n_low, self.l1ext, self.items1, self.items2,
+         self.items3) = [int(v) for v in p]
+
+    def close(self) -> None:
+        if self.h:
+            lib().ora_bsgs_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def bloom(self, level: int, idx: int) -> Bloom:
+        return lib().ora_bsgs_bloom(self.h, level, idx).contents
+
+    def bloom_concat(self, level: int = 1) -> tuple[bytes, int, int, int]:
+        b0 = self.bloom(level, 0)
+        parts = []
+        for i in range(256):
+            b = self.bloom(level, i)
+            parts.append(C.string_at(b.bf, b.bytes))
+        return b"".join(parts), int(b0.bytes), int(b0.bits), int(b0.hashes)
+
+    def giant_table(self) -> bytes:
+        buf = C.create_string_buffer(513 * 64)
+        lib().ora_bsgs_giant_table(self.h, buf)
+        return buf.raw
+
+    def amp_table(self, level: int) -> bytes:
+        buf = C.create_string_buffer(32 * 64)
+        lib().ora_bsgs_amp_table(self.h, level, buf)
+        return buf.raw
+
+    def bptable(self) -> list[tuple[bytes, int]]:
+        t = lib().ora_bsgs_bptable(self.h)
+        return [(bytes(t[i].value), int(t[i].index)) for i in range(self.m3)]
+
+    def chunk_start(self, base: int, target: Point) -> Point:
+        r = Point()
+        lib().ora_bsgs_chunk_start(self.h, C.byref(U256.of(base)), C.byref(target), C.byref(r))
+        return r
+
+    def scan(self, start: Point, j0: int, nj: int, want_x: bool = False, cap: int = 1 << 16):
+        xs = C.create_string_buffer(nj * 1024 * 32) if want_x else None
+        cand = (C.c_uint64 * cap)()
+        n = C.c_uint32(0)
+        nxt = Point()
+        lib().ora_bsgs_scan(self.h, C.byref(start), j0, nj, xs, cand, cap, C.byref(n), C.byref(nxt))
+        return [int(cand[i]) for i in range(min(n.value, cap))], (xs.raw if want_x else None), nxt
+
+    def secondcheck(self, base: int, a: int, target: Point) -> int | None:
+        key = U256()
+        if lib().ora_bsgs_secondcheck(self.h, C.byref(U256.of(base)), a, C.byref(target), C.byref(key)):
+            return key.value()
+        return None
+
+    def search(self, targets: list[Point], start: int, end: int, max_chunks: int = 0):
+        n = len(targets)
+        arr = (Point * n)(*targets)
+        found = (C.c_int * n)()
+        keys = (U256 * n)()
+        chunks = lib().ora_bsgs_search(self.h, arr, n, C.byref(U256.of(start)), C.byref(U256.of(end)), max_chunks,
+                                       found, keys)
+        return int(chunks), [keys[i].value() if found[i] else None for i in range(n)]
+
+    def bench(self, target: Point, base: int, threads: int, seconds: float) -> tuple[int, float]:
+        el = C.c_double(0)
+        steps = lib().ora_bsgs_bench(self.h, C.byref(target), C.byref(U256.of(base)), threads, seconds,
+                                     C.byref(el))
+        return int(steps), float(el.value)
+
+
+# secp256k1 constants (SECP256K1.cpp:31-40)
+P = 2**256 - 2**32 - 977
+ORDER = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
