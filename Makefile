@@ -1,26 +1,45 @@
-# Build everything in-tree (the .so/.bin travel to the GPU box with the repo snapshot).
-#   make            -> keyhuntm1cpu_amd/lib/libkhbsgs.so (HIP, gfx950) + oracle/build/liboracle.so
-HIPCC   ?= /opt/rocm/bin/hipcc
-ARCH    ?= gfx950
-PKG     := keyhuntm1cpu_amd
-CSRC    := $(PKG)/csrc
-LIBDIR  := $(PKG)/lib
+# Build everything in-tree (the .so / binaries travel to the GPU box with the repo snapshot).
+#   keyhuntm1cpu_amd/lib/libkhbsgs.so   HIP giant-step library (gfx950), include/khbsgs.h
+#   keyhuntm1cpu_amd/lib/libkhhost.so   C++ host engine, include/khhost.h
+#   keyhuntm1cpu_amd/bin/keyhunt_amd    keyhunt-compatible CLI (-m bsgs)
+#   oracle/build/liboracle.so           test-only checker (oracle/Makefile)
+HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      ?= g++
+ARCH     ?= gfx950
+PKG      := keyhuntm1cpu_amd
+CSRC     := $(PKG)/csrc
+LIBDIR   := $(PKG)/lib
+BINDIR   := $(PKG)/bin
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wno-unused-result -Wno-unused-value
+CXXFLAGS ?= -O3 -std=c++17 -fPIC -march=x86-64-v3 -Wall -Wextra -Wno-unused-function -Wno-unused-parameter -Wno-unknown-pragmas -pthread
 
-DEV_HDRS := $(wildcard $(CSRC)/device/*.hpp) include/khbsgs.h
+DEV_HDRS  := $(wildcard $(CSRC)/device/*.hpp) include/khbsgs.h
+HOST_SRCS := $(CSRC)/host/u256.cpp $(CSRC)/host/secp_host.cpp $(CSRC)/host/bloom_host.cpp \
+             $(CSRC)/host/bsgs_host.cpp $(CSRC)/host/engine.cpp
+HOST_HDRS := $(wildcard $(CSRC)/host/*.hpp) $(DEV_HDRS) include/khhost.h
+HOST_OBJS := $(patsubst $(CSRC)/host/%.cpp,build/host/%.o,$(HOST_SRCS))
 
-all: $(LIBDIR)/libkhbsgs.so oracle
+all: $(LIBDIR)/libkhbsgs.so $(LIBDIR)/libkhhost.so $(BINDIR)/keyhunt_amd oracle
 
-$(LIBDIR):
+$(LIBDIR) $(BINDIR) build/host:
 	mkdir -p $@
 
 $(LIBDIR)/libkhbsgs.so: $(CSRC)/khbsgs.hip $(DEV_HDRS) | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CSRC)/khbsgs.hip
 
+build/host/%.o: $(CSRC)/host/%.cpp $(HOST_HDRS) | build/host
+	$(CXX) $(CXXFLAGS) -c -o $@ $<
+
+$(LIBDIR)/libkhhost.so: $(HOST_OBJS) build/host/khhost_capi.o $(LIBDIR)/libkhbsgs.so
+	$(CXX) $(CXXFLAGS) -shared -o $@ $(HOST_OBJS) build/host/khhost_capi.o -L$(LIBDIR) -lkhbsgs -Wl,-rpath,'$$ORIGIN'
+
+$(BINDIR)/keyhunt_amd: $(HOST_OBJS) build/host/keyhunt_main.o $(LIBDIR)/libkhbsgs.so | $(BINDIR)
+	$(CXX) $(CXXFLAGS) -o $@ $(HOST_OBJS) build/host/keyhunt_main.o -L$(LIBDIR) -lkhbsgs -Wl,-rpath,'$$ORIGIN/../lib'
+
 oracle:
 	$(MAKE) -s -C oracle
 
 clean:
-	rm -rf $(LIBDIR) oracle/build
+	rm -rf $(LIBDIR) $(BINDIR) build oracle/build
 
 .PHONY: all oracle clean

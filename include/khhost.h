@@ -1,0 +1,67 @@
+/*
+ * khhost.h — C ABI of the host half of the engine, libkhhost.so: keyhunt's BSGS setup and
+ * confirmation (keyhunt.cpp:962-1880, 4271-4368) plus the multi-GPU search driver that calls
+ * libkhbsgs.so.  The keyhunt_amd CLI is built from the same sources; this ABI exists so tests and
+ * bench.py can drive exactly the code the CLI runs.
+ *
+ * Points and 256-bit values cross as big-endian bytes (x||y for points), like include/khbsgs.h.
+ * Functions return 0 on success or a negative KHB_E* code (include/khbsgs.h).
+ */
+#ifndef KHHOST_H
+#define KHHOST_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct khh_tables khh_tables;
+
+/* Geometry + all tables.  n_str: -n value ("0x.." or decimal) or NULL (2^44); k: -k factor;
+ * threads: builder threads; gpl: GPU groups per lane (lane-offset table).  NULL on error (err). */
+khh_tables* khh_tables_new(const char* n_str, int k, int threads, uint32_t gpl, char* err, size_t errlen);
+void khh_tables_free(khh_tables* t);
+/* out: [0]=m [1]=m2 [2]=m3 [3]=aux [4]=cycles [5]=N(low64) [6]=l1 extent [7..9]=bloom entries L1..L3 */
+void khh_params(const khh_tables* t, uint64_t out[10]);
+/* level 1..3, sub-bloom idx 0..255: pointer to the bit array; geometry through the out params */
+const uint8_t* khh_bloom(const khh_tables* t, int level, int idx, uint64_t* bytes, uint64_t* bits, uint32_t* hashes);
+void khh_giant_table(const khh_tables* t, uint8_t out[513 * 64]);
+void khh_amp_table(const khh_tables* t, int level, uint8_t out[32 * 64]);
+uint32_t khh_lane_offsets(const khh_tables* t, uint8_t* out /* n*64, may be NULL */, uint32_t* gpl);
+/* bPtable (sorted): m3 records of {6-byte value, 2 pad, u64 index} */
+const uint8_t* khh_bptable(const khh_tables* t, uint64_t* n);
+
+/* startP of (chunk base, target): keyhunt.cpp:3861-3869 */
+int khh_chunk_centre(const khh_tables* t, const uint8_t base_be[32], const uint8_t target_xy[64], uint8_t out_xy[64]);
+/* bsgs_secondcheck: 1 found (key_be filled), 0 not found */
+int khh_secondcheck(const khh_tables* t, const uint8_t base_be[32], uint32_t a, const uint8_t target_xy[64],
+                    uint8_t key_be[32]);
+
+/* Multi-GPU search over [start, end): found[k] (0/1) and keys[k] (32 B BE) per target.
+ * devices: n_devices device ordinals.  stats_out (nullable): [0]=chunks [1]=giant steps
+ * [2]=candidates [3]=degenerate groups [4]=kernel microseconds [5]=scan launches (stats_out holds 6). */
+int khh_search(const khh_tables* t, const uint8_t* targets_xy, int n_targets, const uint8_t start_be[32],
+               const uint8_t end_be[32], const int* devices, int n_devices, uint32_t lanes,
+               uint32_t chunks_per_batch, uint64_t max_chunks, int* found, uint8_t* keys_be, uint64_t* stats_out,
+               char* err, size_t errlen);
+
+/* Persistent multi-GPU session: contexts opened and tables resident in HBM once, then any number
+ * of searches.  stats_out of khh_session_run: as khh_search plus [5]=scan launches. */
+typedef struct khh_session khh_session;
+khh_session* khh_session_open(const khh_tables* t, const int* devices, int n_devices, uint32_t lanes,
+                              uint32_t chunks_per_batch, int check_threads, char* err, size_t errlen);
+int khh_session_run(khh_session* s, const uint8_t* targets_xy, int n_targets, const uint8_t start_be[32],
+                    const uint8_t end_be[32], uint64_t max_chunks, int random_chunks, int* found, uint8_t* keys_be,
+                    uint64_t* stats_out, char* err, size_t errlen);
+void khh_session_close(khh_session* s);
+
+/* helpers */
+int khh_pubkey(const uint8_t key_be[32], uint8_t out_xy[64]);
+int khh_parse_pubkey(const char* hex, uint8_t out_xy[64], int* compressed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,354 @@
+#include "bsgs_host.hpp"
+
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <mutex>
+#include <thread>
+
+namespace khb {
+
+namespace {
+
+constexpr int kGrp = 1024;      // CPU_GRP_SIZE, keyhunt.cpp:127
+constexpr int kHalf = kGrp / 2;
+constexpr uint64_t kJobKeys = 1048576;    // THREADBPWORKLOAD, keyhunt.cpp:63
+constexpr long double kBloomErr = 0.000001;   // keyhunt.cpp:1238, 1267, 1296
+
+uint64_t items_for(uint64_t m, uint64_t limit) {   // keyhunt.cpp:1185-1213
+  if (m / 256 > limit) return m / 256 + ((m % 256) ? 1 : 0);
+  return 1000;
+}
+
+// One 1024-point group centred on c over stride table tab/tab2 (keyhunt.cpp:4438-4578):
+// xs[t] = x(c + (t - 512) * stride) for t in [0, 1024), then c += 1024 * stride.
+void group_x(Pt& c, const Pt* tab, const Pt& tab2, Fh* xs, Fh* dx, Fh* pre) {
+  for (int i = 0; i < kHalf; ++i) fe_sub(dx[i], tab[i].x, c.x);
+  fe_sub(dx[kHalf], tab2.x, c.x);
+  // Montgomery batch inverse over 513 values (IntGroup.cpp:36-58); a zero product gives 0s.
+  pre[0] = dx[0];
+  for (int i = 1; i <= kHalf; ++i) fe_mul(pre[i], pre[i - 1], dx[i]);
+  Fh inv;
+  fe_inv(inv, pre[kHalf]);
+  for (int i = kHalf; i > 0; --i) {
+    Fh nv;
+    fe_mul(nv, pre[i - 1], inv);
+    fe_mul(inv, inv, dx[i]);
+    dx[i] = nv;
+  }
+  dx[0] = inv;
+  xs[kHalf] = c.x;
+  for (int i = 0; i < kHalf; ++i) {
+    Fh u, s, x;
+    fe_add(u, c.x, tab[i].x);
+    fe_add(s, tab[i].y, c.y);         // c - tab[i]: s^2 = ((tab.y + c.y)/dx)^2
+    fe_mul(s, s, dx[i]);
+    fe_sqr(x, s);
+    fe_sub(xs[kHalf - 1 - i], x, u);
+    if (i < kHalf - 1) {
+      fe_sub(s, tab[i].y, c.y);
+      fe_mul(s, s, dx[i]);
+      fe_sqr(x, s);
+      fe_sub(xs[kHalf + 1 + i], x, u);
+    }
+  }
+  Fh s, nx, ny;
+  fe_sub(s, tab2.y, c.y);
+  fe_mul(s, s, dx[kHalf]);
+  fe_sqr(nx, s);
+  fe_sub(nx, nx, c.x);
+  fe_sub(nx, nx, tab2.x);
+  fe_sub(ny, tab2.x, nx);
+  fe_mul(ny, ny, s);
+  fe_sub(ny, ny, tab2.y);
+  c.x = nx;
+  c.y = ny;
+}
+
+}  // namespace
+
+bool make_geometry(const char* n_str, int kfactor, Geometry& g, std::string& err) {
+  g = Geometry();
+  if (n_str) {
+    bool ok = (n_str[0] == '0' && n_str[1] == 'x') ? U256::from_hex(n_str + 2, g.N) : U256::from_dec(n_str, g.N);
+    if (!ok) { err = "[E] invalid -n value"; return false; }
+  } else {
+    g.N = U256(0x100000000000ull);                      // keyhunt.cpp:1066
+  }
+  // keyhunt.cpp:1069-1076: "exact root" = Euler's criterion mod p; root = ModSqrt mod p.
+  if (g.N >= secp_prime()) { err = "[E] -n param doesn't have exact square root"; return false; }
+  Fh nf = fe_of(g.N), mf;
+  if (!fe_has_sqrt(nf)) { err = "[E] -n param doesn't have exact square root"; return false; }
+  fe_sqrt(mf, nf);
+  g.M = u256_of(mf);
+  U256 r;
+  U256::divmod(g.M, U256(kGrp), nullptr, &r);
+  if (!r.is_zero()) { err = "[E] M value is not divisible by 1024"; return false; }
+  // keyhunt.cpp:1129-1179
+  g.M = g.M * (uint64_t)(kfactor <= 0 ? 1 : kfactor);
+  U256::divmod(g.M, U256(32), &g.M2, &r);
+  if (!r.is_zero()) g.M2 = g.M2 + U256(1);
+  g.M_double = g.M * 2ull;
+  g.M2_double = g.M2 * 2ull;
+  U256::divmod(g.M2, U256(32), &g.M3, &r);
+  if (!r.is_zero()) g.M3 = g.M3 + U256(1);
+  g.M3_double = g.M3 * 2ull;
+  U256 aux;
+  U256::divmod(g.N, g.M, &aux, &r);
+  if (!r.is_zero()) g.N = g.M * aux;
+  g.N_double = g.N * 2ull;
+  if (!g.M.fits64() || g.M.w[0] > (1ull << 40) || !aux.fits64()) {
+    err = "[E] baby-step table too large";
+    return false;
+  }
+  g.m = g.M.w[0];
+  g.m2 = g.M2.w[0];
+  g.m3 = g.M3.w[0];
+  g.aux = aux.w[0];
+  g.items1 = items_for(g.m, 10000);
+  g.items2 = items_for(g.m2, 1000);
+  g.items3 = items_for(g.m3, 1000);
+  g.cycles = g.aux / kGrp + ((g.aux % kGrp) ? 1 : 0);     // keyhunt.cpp:3810-3813
+  g.intaux = g.M_double * (uint64_t)kHalf + g.M;           // keyhunt.cpp:3815-3817
+  // L1 extent: the last 2^20-key build job's `to` overshoots m by one job when m is not a
+  // multiple of the job size (keyhunt.cpp:1739-1793 with thread_bPload's "i_counter < to").
+  uint64_t W = kJobKeys >= g.m ? g.m : kJobKeys;
+  uint64_t R = g.m % W;
+  g.l1ext = R ? (g.m / W) * W + W + R : g.m;
+  return true;
+}
+
+bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, std::string& err,
+                   const std::function<void(uint64_t, uint64_t)>& progress) {
+  geo = g;
+  l1.assign(256, BloomFilter());
+  l2.assign(256, BloomFilter());
+  l3.assign(256, BloomFilter());
+  for (int i = 0; i < 256; ++i) {
+    if (l1[i].init2(g.items1, kBloomErr) || l2[i].init2(g.items2, kBloomErr) || l3[i].init2(g.items3, kBloomErr)) {
+      err = "[E] error bloom_init";
+      return false;
+    }
+  }
+  bp.assign(g.m3, XValue());
+  // giant tables (keyhunt.cpp:1309-1364)
+  {
+    Pt bsP = negation(mul_g(g.M_double));
+    Pt q = bsP;
+    gsn[0] = q;
+    q = double_direct(q);
+    gsn[1] = q;
+    for (int i = 2; i < kHalf; ++i) { q = add_direct(q, bsP); gsn[i] = q; }
+    g2sn = double_direct(gsn[kHalf - 1]);
+    Pt t;
+    amp2[0] = negation(mul_g(g.M2));
+    t = negation(mul_g(g.M2_double));
+    for (int i = 1; i < 32; ++i) amp2[i] = add_direct(amp2[i - 1], t);
+    amp3[0] = negation(mul_g(g.M3));
+    t = negation(mul_g(g.M3_double));
+    for (int i = 1; i < 32; ++i) amp3[i] = add_direct(amp3[i - 1], t);
+  }
+  // lane offsets for the GPU: offs[m] = (m * gpl) * _2GSn = -(m * gpl * 2048 * M) * G
+  gpl = groups_per_lane ? groups_per_lane : 1;
+  const uint64_t n_off = (g.cycles + gpl - 1) / gpl;
+  lane_offs.assign(n_off, Pt());
+  // baby-step stride table Gn (init_generator, keyhunt.cpp:4386-4399)
+  std::vector<Pt> gn(kHalf);
+  Pt g2n;
+  {
+    Pt q = secp_g();
+    gn[0] = q;
+    q = double_direct(q);
+    gn[1] = q;
+    for (int i = 2; i < kHalf; ++i) { q = add_direct(q, secp_g()); gn[i] = q; }
+    g2n = double_direct(gn[kHalf - 1]);
+  }
+  // build jobs (keyhunt.cpp:1739-1807): [from, to) of 2^20 keys, last job overshooting (quirk vi)
+  struct Job { uint64_t from, to; };
+  std::vector<Job> jobs;
+  {
+    uint64_t W = kJobKeys >= g.m ? g.m : kJobKeys;
+    uint64_t cyc = g.m / W, R = g.m % W;
+    if (R) cyc++;
+    uint64_t base = 0;
+    for (uint64_t j = 0; j < cyc; ++j) {
+      jobs.push_back({base, j < cyc - 1 ? base + W : base + W + R});
+      base += W;
+    }
+  }
+  if (nthreads < 1) nthreads = 1;
+  std::atomic<uint64_t> next_job{0}, next_off{1}, done{0};
+  std::atomic<int> finished{0};
+  auto worker = [&]() {
+    std::vector<Fh> xs(kGrp), dx(kHalf + 1), pre(kHalf + 1);
+    uint8_t xb[32];
+    for (;;) {
+      const uint64_t j = next_job.fetch_add(1);
+      if (j >= jobs.size()) break;
+      const uint64_t from = jobs[j].from, to = jobs[j].to;
+      const uint64_t nb = (to - from) / kGrp + (((to - from) % kGrp) ? 1 : 0);
+      Pt c = mul_g(U256(from + 1 + kHalf));
+      uint64_t ic = from;
+      for (uint64_t s = 0; s < nb; ++s) {
+        group_x(c, gn.data(), g2n, xs.data(), dx.data(), pre.data());
+        for (int t = 0; t < kGrp; ++t, ++ic) {
+          fe_to_be(xb, xs[t]);
+          const int idx = xb[0];
+          if (ic < g.m3) {
+            memcpy(bp[ic].value, xb + 16, 6);
+            bp[ic].index = ic;
+            l3[idx].add32_atomic(xb);
+          }
+          if (ic < g.m2) l2[idx].add32_atomic(xb);
+          if (ic < to) l1[idx].add32_atomic(xb);
+        }
+        done.fetch_add(kGrp);
+      }
+    }
+    // lane offsets share the pool
+    for (;;) {
+      const uint64_t m = next_off.fetch_add(1);
+      if (m >= n_off) break;
+      lane_offs[m] = negation(mul_g(g.M_double * (uint64_t)(m * gpl * kHalf * 2)));
+    }
+    finished.fetch_add(1);
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t) th.emplace_back(worker);
+  while (progress && finished.load() < nthreads) {
+    progress(done.load(), g.l1ext);
+    std::this_thread::sleep_for(std::chrono::milliseconds(250));
+  }
+  for (auto& x : th) x.join();
+  if (progress) progress(g.l1ext, g.l1ext);
+  // bsgs_sort (keyhunt.cpp:3657-3746): for distinct 6-byte keys any correct sort gives the same
+  // array; equal keys (SURVEY §8a quirk v) are ordered by index here.
+  std::sort(bp.begin(), bp.end(), [](const XValue& a, const XValue& b) {
+    int r = memcmp(a.value, b.value, 6);
+    return r ? r < 0 : a.index < b.index;
+  });
+  return true;
+}
+
+std::vector<uint8_t> Tables::l1_concat() const {
+  std::vector<uint8_t> out(256 * l1[0].bytes);
+  for (int i = 0; i < 256; ++i) memcpy(out.data() + i * l1[0].bytes, l1[i].bf.data(), l1[0].bytes);
+  return out;
+}
+
+std::vector<uint8_t> Tables::giant_table_be() const {
+  std::vector<uint8_t> out(513 * 64);
+  for (int i = 0; i < kHalf; ++i) pt_to_be(out.data() + 64 * i, gsn[i]);
+  pt_to_be(out.data() + 64 * kHalf, g2sn);
+  return out;
+}
+
+std::vector<uint8_t> Tables::lane_offsets_be() const {
+  std::vector<uint8_t> out(64 * lane_offs.size());
+  for (size_t i = 0; i < lane_offs.size(); ++i) pt_to_be(out.data() + 64 * i, lane_offs[i]);
+  return out;
+}
+
+Pt Tables::chunk_aux(const U256& base) const {
+  U256 km = secp_order() - base - geo.intaux;
+  return mul_g(km);
+}
+
+void batch_add_direct(const Pt* targets, const Pt& aux, size_t n, Pt* out) {
+  std::vector<Fh> dx(n), pre(n);
+  for (size_t k = 0; k < n; ++k) fe_sub(dx[k], aux.x, targets[k].x);
+  fe_batch_inv(dx.data(), n, pre.data());
+  for (size_t k = 0; k < n; ++k) {
+    Fh dy, s, p;
+    Pt r;
+    fe_sub(dy, aux.y, targets[k].y);
+    fe_mul(s, dy, dx[k]);
+    fe_sqr(p, s);
+    fe_sub(r.x, p, targets[k].x);
+    fe_sub(r.x, r.x, aux.x);
+    fe_sub(r.y, aux.x, r.x);
+    fe_mul(r.y, r.y, s);
+    fe_sub(r.y, r.y, aux.y);
+    out[k] = r;
+  }
+}
+
+bool Tables::searchbinary(const uint8_t* x, uint64_t& idx) const {
+  // bsgs_searchbinary (keyhunt.cpp:3748-3773): probes bytes 16..21 of x
+  int64_t lo = 0, hi = (int64_t)bp.size() - 1;
+  while (lo <= hi) {
+    int64_t mid = lo + (hi - lo) / 2;
+    int r = memcmp(x + 16, bp[mid].value, 6);
+    if (r == 0) { idx = bp[mid].index; return true; }
+    if (r < 0) hi = mid - 1; else lo = mid + 1;
+  }
+  return false;
+}
+
+static U256 calc_index(const Geometry& g, uint32_t i) {   // calcualteindex, keyhunt.cpp:6680-6689
+  return g.M3_double * (uint64_t)i + g.M3;
+}
+
+// AddDirect(q, tab[i]) for i < 32 with one shared inversion (same values as 32 separate
+// AddDirects, incl. dx == 0 -> inverse 0).
+static void add_direct_32(const Pt& q, const Pt* tab, Pt* out) {
+  Fh dx[32], pre[32];
+  for (int i = 0; i < 32; ++i) fe_sub(dx[i], tab[i].x, q.x);
+  fe_batch_inv(dx, 32, pre);
+  for (int i = 0; i < 32; ++i) {
+    Fh dy, s, p;
+    fe_sub(dy, tab[i].y, q.y);
+    fe_mul(s, dy, dx[i]);
+    fe_sqr(p, s);
+    fe_sub(out[i].x, p, q.x);
+    fe_sub(out[i].x, out[i].x, tab[i].x);
+    fe_sub(out[i].y, tab[i].x, out[i].x);
+    fe_mul(out[i].y, out[i].y, s);
+    fe_sub(out[i].y, out[i].y, tab[i].y);
+  }
+}
+
+bool Tables::thirdcheck(const U256& start, uint32_t a, const Pt& target, U256& key) const {
+  U256 base = geo.M2_double * (uint64_t)a + start;
+  const Pt Q = add_direct(target, negation(mul_g(base)));
+  Pt S32[32];
+  add_direct_32(Q, amp3, S32);
+  uint8_t xb[32];
+  for (int i = 0; i < 32; ++i) {
+    const Pt& S = S32[i];
+    fe_to_be(xb, S.x);
+    if (l3[xb[0]].check32(xb)) {
+      uint64_t j = 0;
+      if (searchbinary(xb, j)) {
+        const U256 ci = calc_index(geo, (uint32_t)i);
+        key = ci + U256(j + 1) + base;
+        if (fe_eq(mul_g(key).x, target.x)) return true;
+        key = ci - U256(j + 1) + base;
+        if (fe_eq(mul_g(key).x, target.x)) return true;
+      }
+    } else if (fe_eq(Q.x, amp3[i].x)) {        // AddDirect(P,-P) special case, keyhunt.cpp:4352-4364
+      key = calc_index(geo, (uint32_t)i) + base;
+      return true;
+    }
+  }
+  return false;
+}
+
+bool Tables::secondcheck(const U256& start, uint32_t a, const Pt& target, U256& key) const {
+  U256 base = geo.M_double * (uint64_t)a + start;
+  const Pt Q = add_direct(target, negation(mul_g(base)));
+  Pt S32[32];
+  add_direct_32(Q, amp2, S32);
+  uint8_t xb[32];
+  for (int i = 0; i < 32; ++i) {
+    fe_to_be(xb, S32[i].x);
+    if (l2[xb[0]].check32(xb)) {
+      if (thirdcheck(base, (uint32_t)i, target, key)) return true;
+    }
+  }
+  return false;
+}
+
+}  // namespace khb

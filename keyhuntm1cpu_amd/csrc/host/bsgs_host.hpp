@@ -1,0 +1,64 @@
+// BSGS host engine: everything of keyhunt's `-m bsgs` except the giant-step scan itself, which
+// runs on the GPU through libkhbsgs (include/khbsgs.h).
+//
+//   geometry      keyhunt.cpp:1045-1213   (N, M = sqrt(N)*k, M2, M3, aux, bloom entry counts)
+//   giant tables  keyhunt.cpp:1309-1364   (GSn, _2GSn, AMP2, AMP3)
+//   baby tables   keyhunt.cpp:1615-1880 + thread_bPload 4404-4592 (3-level blooms, bPtable)
+//   chunk centre  keyhunt.cpp:3861-3869
+//   confirmation  bsgs_secondcheck/thirdcheck 4271-4368, bsgs_searchbinary 3748-3773,
+//                 calcualteindex 6680-6689
+#pragma once
+#include <stdint.h>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "bloom_host.hpp"
+#include "secp_host.hpp"
+#include "u256.hpp"
+
+namespace khb {
+
+struct Geometry {
+  U256 N, M, M2, M3, M_double, M2_double, M3_double, N_double, intaux;
+  uint64_t m = 0, m2 = 0, m3 = 0, aux = 0, cycles = 0, l1ext = 0;
+  uint64_t items1 = 0, items2 = 0, items3 = 0;
+};
+
+// n_str: the -n argument ("0x..." hex or decimal) or nullptr for the default 2^44.
+bool make_geometry(const char* n_str, int kfactor, Geometry& g, std::string& err);
+
+struct XValue {            // struct bsgs_xvalue, keyhunt.cpp:70-73
+  uint8_t value[6];
+  uint8_t pad[2];
+  uint64_t index;
+};
+
+struct Tables {
+  Geometry geo;
+  std::vector<BloomFilter> l1, l2, l3;   // 256 sub-blooms each
+  std::vector<XValue> bp;                // sorted by value (bsgs_sort)
+  Pt gsn[512], g2sn, amp2[32], amp3[32];
+  uint32_t gpl = 0;                      // GPU groups per lane
+  std::vector<Pt> lane_offs;             // offs[m] = (m*gpl) * _2GSn
+
+  // progress(done, total) is called from the builder threads' coordinator.
+  bool build(const Geometry& g, int nthreads, uint32_t groups_per_lane, std::string& err,
+             const std::function<void(uint64_t, uint64_t)>& progress = nullptr);
+  std::vector<uint8_t> l1_concat() const;
+  std::vector<uint8_t> giant_table_be() const;
+  std::vector<uint8_t> lane_offsets_be() const;
+
+  // (order - base - intaux) * G, shared by every target of a chunk (keyhunt.cpp:3862-3866)
+  Pt chunk_aux(const U256& base) const;
+  bool secondcheck(const U256& base, uint32_t a, const Pt& target, U256& key) const;
+
+ private:
+  bool thirdcheck(const U256& base2, uint32_t i2, const Pt& target, U256& key) const;
+  bool searchbinary(const uint8_t* x, uint64_t& idx) const;
+};
+
+// Batched chunk centres: out[k] = AddDirect(targets[k], aux) with one shared inversion.
+void batch_add_direct(const Pt* targets, const Pt& aux, size_t n, Pt* out);
+
+}  // namespace khb

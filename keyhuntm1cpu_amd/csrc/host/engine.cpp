@@ -1,0 +1,298 @@
+#include "engine.hpp"
+
+#include <string.h>
+#include <sys/random.h>
+
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <thread>
+
+#include "../../../include/khbsgs.h"
+
+namespace khb {
+
+namespace {
+
+template <class F>
+void parallel_for(size_t n, int threads, F&& fn) {
+  if (n == 0) return;
+  if (threads <= 1 || n < 2) {
+    for (size_t i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  auto body = [&]() {
+    for (;;) {
+      size_t i = next.fetch_add(1);
+      if (i >= n) break;
+      fn(i);
+    }
+  };
+  std::vector<std::thread> th;
+  const int nt = (int)std::min<size_t>((size_t)threads, n);
+  for (int t = 1; t < nt; ++t) th.emplace_back(body);
+  body();
+  for (auto& t : th) t.join();
+}
+
+// Uniform random value in [lo, hi) (the -B random chunk policy; Int::Rand, Int.cpp:751-765).
+U256 random_in(const U256& lo, const U256& hi) {
+  U256 span = hi - lo, v, r;
+  uint8_t b[32];
+  if (getrandom(b, sizeof b, 0) != (ssize_t)sizeof b) memset(b, 0x5a, sizeof b);
+  v = U256::from_be(b);
+  if (span.is_zero()) return lo;
+  U256::divmod(v, span, nullptr, &r);
+  return lo + r;
+}
+
+struct Shared {
+  const Tables& T;
+  const std::vector<Target>& targets;
+  const SearchConfig& cfg;
+  const SearchCallbacks& cb;
+  U256 start, end, cursor;
+  std::mutex mu;            // cursor, found, keys, stats, callbacks
+  std::vector<int>& found;
+  std::vector<U256>& keys;
+  SearchStats& stats;
+  uint64_t claimed = 0;
+  int n_found = 0;
+  bool stop = false;
+  int error = 0;
+  std::string err;
+
+  Shared(const Tables& t, const std::vector<Target>& tg, const SearchConfig& c, const SearchCallbacks& b,
+         std::vector<int>& f, std::vector<U256>& k, SearchStats& s)
+      : T(t), targets(tg), cfg(c), cb(b), found(f), keys(k), stats(s) {}
+};
+
+struct Batch {
+  std::vector<U256> bases;        // chunk bases, in claim order
+  std::vector<uint32_t> job_chunk, job_target;
+  std::vector<uint8_t> centres;   // 64 B per job
+};
+
+bool claim(Shared& S, uint32_t want, Batch& b) {
+  std::lock_guard<std::mutex> lk(S.mu);
+  b.bases.clear();
+  for (uint32_t i = 0; i < want && !S.stop; ++i) {
+    if (S.cfg.max_chunks && S.claimed >= S.cfg.max_chunks) break;
+    U256 base;
+    if (S.cfg.random_chunks) {
+      base = random_in(S.start, S.end);
+    } else {
+      base = S.cursor;
+      if (base >= S.end) break;            // keyhunt.cpp:3843-3844
+      S.cursor = S.cursor + S.T.geo.N_double;
+    }
+    b.bases.push_back(base);
+    S.claimed++;
+    if (S.cb.on_chunk) S.cb.on_chunk(base);
+  }
+  return !b.bases.empty();
+}
+
+// Centres of every (chunk, live target) job: target + (order - base - intaux)*G.
+void make_jobs(Shared& S, Batch& b, int threads) {
+  std::vector<int> live;
+  {
+    std::lock_guard<std::mutex> lk(S.mu);
+    for (size_t k = 0; k < S.targets.size(); ++k)
+      if (!S.found[k]) live.push_back((int)k);
+  }
+  const size_t nc = b.bases.size(), nt = live.size();
+  b.job_chunk.resize(nc * nt);
+  b.job_target.resize(nc * nt);
+  b.centres.resize(64 * nc * nt);
+  std::vector<Pt> tp(nt);
+  for (size_t j = 0; j < nt; ++j) tp[j] = S.targets[live[j]].p;
+  parallel_for(nc, threads, [&](size_t c) {
+    const Pt aux = S.T.chunk_aux(b.bases[c]);
+    std::vector<Pt> out(nt);
+    batch_add_direct(tp.data(), aux, nt, out.data());
+    for (size_t j = 0; j < nt; ++j) {
+      const size_t job = c * nt + j;
+      b.job_chunk[job] = (uint32_t)c;
+      b.job_target[job] = (uint32_t)live[j];
+      pt_to_be(b.centres.data() + 64 * job, out[j]);
+    }
+  });
+}
+
+// Confirm level-1 candidates (bsgs_secondcheck, keyhunt.cpp:3947-3982): speculative parallel
+// checks, then in-order resolution.
+void confirm(Shared& S, const Batch& b, std::vector<khb_cand>& cands, int threads) {
+  std::sort(cands.begin(), cands.end(), [](const khb_cand& x, const khb_cand& y) {
+    return x.job != y.job ? x.job < y.job : x.a < y.a;
+  });
+  std::vector<int> ok(cands.size(), 0);
+  std::vector<U256> key(cands.size());
+  std::vector<int> found_snapshot;
+  {
+    std::lock_guard<std::mutex> lk(S.mu);
+    found_snapshot = S.found;
+  }
+  parallel_for(cands.size(), threads, [&](size_t i) {
+    const uint32_t job = cands[i].job;
+    const uint32_t k = b.job_target[job];
+    if (found_snapshot[k]) return;
+    ok[i] = S.T.secondcheck(b.bases[b.job_chunk[job]], cands[i].a, S.targets[k].p, key[i]) ? 1 : 0;
+  });
+  std::lock_guard<std::mutex> lk(S.mu);
+  for (size_t i = 0; i < cands.size(); ++i) {
+    if (!ok[i]) continue;
+    const uint32_t k = b.job_target[cands[i].job];
+    if (S.found[k]) continue;
+    S.found[k] = 1;
+    S.keys[k] = key[i];
+    S.n_found++;
+    if (S.cb.on_found) S.cb.on_found((int)k, key[i]);
+  }
+  if (S.n_found == (int)S.targets.size()) S.stop = true;   // "All points were found"
+}
+
+uint32_t batch_chunks(const Tables& T, const SearchConfig& cfg, size_t ntargets) {
+  if (cfg.chunks_per_batch) return cfg.chunks_per_batch;
+  const uint64_t lanes_per_job = (T.geo.cycles + T.gpl - 1) / T.gpl;
+  const uint64_t lanes = cfg.lanes ? cfg.lanes : 256u * 8u * 64u;
+  const uint64_t jobs = (2ull * lanes + lanes_per_job - 1) / lanes_per_job;    // ~2 work items per lane
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(jobs / std::max<size_t>(1, ntargets), 65536));
+}
+
+// One device: claim/centre the next batch and confirm the previous one while the GPU scans.
+void device_thread(Shared& S, khb_ctx* ctx) {
+  auto fail = [&](int rc, const char* what) {
+    std::lock_guard<std::mutex> lk(S.mu);
+    if (!S.error) {
+      S.error = rc;
+      S.err = std::string("[E] ") + what + ": " + khb_strerror(rc);
+    }
+    S.stop = true;
+  };
+  const Tables& T = S.T;
+  const uint32_t cycles = (uint32_t)T.geo.cycles;
+  const uint32_t want = batch_chunks(T, S.cfg, S.targets.size());
+  const int threads = S.cfg.check_threads > 0 ? S.cfg.check_threads
+                                               : (int)std::max(2u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<khb_cand> cbuf(1u << 20);
+  std::vector<khb_degenerate> dbuf(4096);
+  Batch bat[3];
+  int cur = 0, nxt = 1, prv = 2;
+  std::vector<khb_cand> prev_cands;
+  bool have_prev = false;
+  auto stopped = [&]() { std::lock_guard<std::mutex> lk(S.mu); return S.stop; };
+  auto prepare = [&](Batch& b) {
+    if (stopped() || !claim(S, want, b)) return false;
+    make_jobs(S, b, threads);
+    return !b.job_chunk.empty();
+  };
+  bool have_cur = prepare(bat[cur]);
+  int rc = 0;
+  if (have_cur) {
+    rc = khb_submit(ctx, bat[cur].centres.data(), (uint32_t)bat[cur].job_chunk.size(), 0, cycles);
+    if (rc) { fail(rc, "khb_submit"); return; }
+  }
+  while (have_cur) {
+    const bool have_next = prepare(bat[nxt]);                  // overlaps the GPU scan of cur
+    if (have_prev) confirm(S, bat[prv], prev_cands, threads);  // overlaps the GPU scan of cur
+    have_prev = false;
+    khb_stats st{};
+    rc = khb_collect(ctx, cbuf.data(), (uint32_t)cbuf.size(), dbuf.data(), (uint32_t)dbuf.size(), &st);
+    if (rc) { fail(rc, "khb_collect"); return; }
+    if (have_next) {
+      rc = khb_submit(ctx, bat[nxt].centres.data(), (uint32_t)bat[nxt].job_chunk.size(), 0, cycles);
+      if (rc) { fail(rc, "khb_submit"); return; }
+    }
+    if (st.n_cand > cbuf.size()) { fail(KHB_ENOMEM, "candidate buffer overflow (lower the batch size)"); return; }
+    {
+      std::lock_guard<std::mutex> lk(S.mu);
+      S.stats.launches += 1;
+      S.stats.chunks += bat[cur].bases.size();
+      S.stats.giant_steps += st.giant_steps;
+      S.stats.candidates += st.n_cand;
+      S.stats.degenerate += st.n_degenerate;
+      S.stats.kernel_seconds += st.kernel_ms * 1e-3;
+      for (uint32_t i = 0; i < st.n_degenerate && i < dbuf.size(); ++i) {
+        if (!S.cb.on_warning) break;
+        const uint32_t job = dbuf[i].job;
+        S.cb.on_warning("[W] collapsed batch inverse (target on a window centre): chunk 0x" +
+                        bat[cur].bases[bat[cur].job_chunk[job]].hex() + " group " +
+                        std::to_string(dbuf[i].group & 0x7fffffffu));
+      }
+    }
+    prev_cands.assign(cbuf.begin(), cbuf.begin() + st.n_cand);
+    have_prev = true;
+    const int old_prv = prv;
+    prv = cur;
+    cur = nxt;
+    nxt = old_prv;
+    have_cur = have_next;
+  }
+  if (have_prev) confirm(S, bat[prv], prev_cands, threads);
+}
+
+}  // namespace
+
+int Session::open(const Tables& T, const SearchConfig& cfg, std::string& err) {
+  close();
+  T_ = &T;
+  cfg_ = cfg;
+  std::vector<uint8_t> bf = T.l1_concat();
+  std::vector<uint8_t> gsn = T.giant_table_be();
+  std::vector<uint8_t> offs = T.lane_offsets_be();
+  for (int d : cfg.devices) {
+    khb_ctx* c = nullptr;
+    int rc = khb_open(d, cfg.lanes, &c);
+    if (!rc) rc = khb_load_bloom(c, bf.data(), T.l1[0].bytes, T.l1[0].bits, T.l1[0].hashes);
+    if (!rc) rc = khb_load_giant_table(c, gsn.data());
+    if (!rc) rc = khb_load_lane_offsets(c, offs.data(), (uint32_t)T.lane_offs.size(), T.gpl);
+    if (rc) {
+      err = "[E] GPU " + std::to_string(d) + ": " + khb_strerror(rc);
+      if (c) khb_close(c);
+      close();
+      return rc;
+    }
+    ctx_.push_back(c);
+  }
+  return 0;
+}
+
+void Session::close() {
+  for (void* c : ctx_) khb_close((khb_ctx*)c);
+  ctx_.clear();
+}
+
+int Session::run(const std::vector<Target>& targets, const U256& start, const U256& end, const SearchCallbacks& cb,
+                 std::vector<int>& found, std::vector<U256>& keys, SearchStats& stats, std::string& err,
+                 uint64_t max_chunks, bool random_chunks) {
+  found.assign(targets.size(), 0);
+  keys.assign(targets.size(), U256());
+  stats = SearchStats();
+  if (targets.empty()) { err = "[E] no targets"; return KHB_EINVAL; }
+  if (ctx_.empty() || !T_) { err = "[E] session not open"; return KHB_ESTATE; }
+  SearchConfig cfg = cfg_;
+  cfg.max_chunks = max_chunks;
+  cfg.random_chunks = random_chunks;
+  Shared S(*T_, targets, cfg, cb, found, keys, stats);
+  S.start = start;
+  S.end = end;
+  S.cursor = start;
+  std::vector<std::thread> th;
+  for (void* c : ctx_) th.emplace_back(device_thread, std::ref(S), (khb_ctx*)c);
+  for (auto& t : th) t.join();
+  if (S.error) err = S.err;
+  return S.error;
+}
+
+int run_search(const Tables& T, const std::vector<Target>& targets, const U256& start, const U256& end,
+               const SearchConfig& cfg, const SearchCallbacks& cb, std::vector<int>& found, std::vector<U256>& keys,
+               SearchStats& stats, std::string& err) {
+  Session s;
+  int rc = s.open(T, cfg, err);
+  if (rc) return rc;
+  return s.run(targets, start, end, cb, found, keys, stats, err, cfg.max_chunks, cfg.random_chunks);
+}
+
+}  // namespace khb

@@ -1,0 +1,78 @@
+// Search driver: the role of keyhunt.cpp's thread_process_bsgs workers (3778-4009) and the chunk
+// scheduler (BSGS_CURRENT += 2N under a mutex, 3824-3844), re-shaped for GPUs:
+//   - one host thread per device owns a libkhbsgs context;
+//   - a thread claims a batch of consecutive chunks, computes every (chunk, target) centre with a
+//     batched AddDirect, submits the batch, and while the GPU scans it confirms the previous
+//     batch's level-1 candidates on a CPU pool (bsgs_secondcheck/thirdcheck);
+//   - confirmations run speculatively in parallel and are resolved in (chunk, target, a) order, so
+//     the found keys are those a sequential `-t 1` reference run reports.
+#pragma once
+#include <stdint.h>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "bsgs_host.hpp"
+
+namespace khb {
+
+struct Target {
+  Pt p;
+  bool compressed = true;
+};
+
+struct SearchConfig {
+  std::vector<int> devices{0};
+  uint32_t lanes = 0;              // per device, 0 = library default
+  uint32_t chunks_per_batch = 0;   // 0 = auto (fill the device)
+  int check_threads = 0;           // CPU confirmation pool, 0 = auto
+  uint64_t max_chunks = 0;         // 0 = until range end
+  bool random_chunks = false;      // -B random: every chunk base drawn uniformly in the range
+};
+
+struct SearchStats {
+  uint64_t launches = 0;           // GPU scan launches (one per batch per device)
+  uint64_t chunks = 0;
+  uint64_t giant_steps = 0;
+  uint64_t candidates = 0;
+  uint64_t degenerate = 0;
+  double kernel_seconds = 0;       // summed over devices
+};
+
+struct SearchCallbacks {
+  // key found for target k (called in order, under the engine's report lock)
+  std::function<void(int k, const U256& key)> on_found;
+  // progress: base of the chunk a device just claimed (for `-q`-less "Thread 0x..." lines)
+  std::function<void(const U256& base)> on_chunk;
+  std::function<void(const std::string& msg)> on_warning;
+};
+
+// A set of opened devices with the tables resident in HBM (libkhbsgs contexts), reusable across
+// searches.  The CLI opens one; bench.py times run() on an open session.
+class Session {
+ public:
+  Session() = default;
+  ~Session() { close(); }
+  Session(const Session&) = delete;
+  Session& operator=(const Session&) = delete;
+  int open(const Tables& T, const SearchConfig& cfg, std::string& err);
+  int run(const std::vector<Target>& targets, const U256& start, const U256& end, const SearchCallbacks& cb,
+          std::vector<int>& found, std::vector<U256>& keys, SearchStats& stats, std::string& err,
+          uint64_t max_chunks = 0, bool random_chunks = false);
+  void close();
+  const SearchConfig& config() const { return cfg_; }
+
+ private:
+  const Tables* T_ = nullptr;
+  SearchConfig cfg_;
+  std::vector<void*> ctx_;   // khb_ctx*
+};
+
+// Runs the search over [start, end) on a temporary session.  Returns 0, or a negative khbsgs error code.  found/keys are
+// sized to targets.size().  stats is updated live (read it from another thread for the
+// periodic "Total ... keys" line).
+int run_search(const Tables& T, const std::vector<Target>& targets, const U256& start, const U256& end,
+               const SearchConfig& cfg, const SearchCallbacks& cb, std::vector<int>& found, std::vector<U256>& keys,
+               SearchStats& stats, std::string& err);
+
+}  // namespace khb

@@ -1,0 +1,182 @@
+// libkhhost.so: C ABI over the host engine (include/khhost.h).
+#include <string.h>
+
+#include <string>
+#include <thread>
+
+#include "../../../include/khbsgs.h"
+#include "../../../include/khhost.h"
+#include "bsgs_host.hpp"
+#include "engine.hpp"
+
+using namespace khb;
+
+struct khh_tables {
+  Tables t;
+};
+
+static void set_err(char* err, size_t n, const std::string& m) {
+  if (err && n) {
+    strncpy(err, m.c_str(), n - 1);
+    err[n - 1] = 0;
+  }
+}
+
+extern "C" {
+
+khh_tables* khh_tables_new(const char* n_str, int k, int threads, uint32_t gpl, char* err, size_t errlen) {
+  Geometry g;
+  std::string e;
+  if (!make_geometry(n_str, k, g, e)) { set_err(err, errlen, e); return nullptr; }
+  khh_tables* t = new khh_tables();
+  if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
+  if (!t->t.build(g, threads, gpl ? gpl : 4, e)) {
+    set_err(err, errlen, e);
+    delete t;
+    return nullptr;
+  }
+  return t;
+}
+
+void khh_tables_free(khh_tables* t) { delete t; }
+
+void khh_params(const khh_tables* t, uint64_t out[10]) {
+  const Geometry& g = t->t.geo;
+  out[0] = g.m; out[1] = g.m2; out[2] = g.m3; out[3] = g.aux; out[4] = g.cycles;
+  out[5] = g.N.w[0]; out[6] = g.l1ext; out[7] = g.items1; out[8] = g.items2; out[9] = g.items3;
+}
+
+const uint8_t* khh_bloom(const khh_tables* t, int level, int idx, uint64_t* bytes, uint64_t* bits, uint32_t* hashes) {
+  if (idx < 0 || idx > 255 || level < 1 || level > 3) return nullptr;
+  const BloomFilter& b = level == 1 ? t->t.l1[idx] : level == 2 ? t->t.l2[idx] : t->t.l3[idx];
+  if (bytes) *bytes = b.bytes;
+  if (bits) *bits = b.bits;
+  if (hashes) *hashes = b.hashes;
+  return b.bf.data();
+}
+
+void khh_giant_table(const khh_tables* t, uint8_t out[513 * 64]) {
+  std::vector<uint8_t> v = t->t.giant_table_be();
+  memcpy(out, v.data(), v.size());
+}
+
+void khh_amp_table(const khh_tables* t, int level, uint8_t out[32 * 64]) {
+  const Pt* a = level == 2 ? t->t.amp2 : t->t.amp3;
+  for (int i = 0; i < 32; ++i) pt_to_be(out + 64 * i, a[i]);
+}
+
+uint32_t khh_lane_offsets(const khh_tables* t, uint8_t* out, uint32_t* gpl) {
+  if (gpl) *gpl = t->t.gpl;
+  if (out) {
+    std::vector<uint8_t> v = t->t.lane_offsets_be();
+    memcpy(out, v.data(), v.size());
+  }
+  return (uint32_t)t->t.lane_offs.size();
+}
+
+const uint8_t* khh_bptable(const khh_tables* t, uint64_t* n) {
+  static_assert(sizeof(XValue) == 16, "bsgs_xvalue is 16 bytes");
+  if (n) *n = t->t.bp.size();
+  return reinterpret_cast<const uint8_t*>(t->t.bp.data());
+}
+
+int khh_chunk_centre(const khh_tables* t, const uint8_t base_be[32], const uint8_t target_xy[64], uint8_t out_xy[64]) {
+  const U256 base = U256::from_be(base_be);
+  const Pt tg = pt_from_be(target_xy);
+  const Pt aux = t->t.chunk_aux(base);
+  Pt c;
+  batch_add_direct(&tg, aux, 1, &c);
+  pt_to_be(out_xy, c);
+  return 0;
+}
+
+int khh_secondcheck(const khh_tables* t, const uint8_t base_be[32], uint32_t a, const uint8_t target_xy[64],
+                    uint8_t key_be[32]) {
+  U256 key;
+  if (!t->t.secondcheck(U256::from_be(base_be), a, pt_from_be(target_xy), key)) return 0;
+  key.to_be(key_be);
+  return 1;
+}
+
+struct khh_session {
+  Session s;
+};
+
+khh_session* khh_session_open(const khh_tables* t, const int* devices, int n_devices, uint32_t lanes,
+                              uint32_t chunks_per_batch, int check_threads, char* err, size_t errlen) {
+  if (!t || !devices || n_devices <= 0) { set_err(err, errlen, "[E] bad arguments"); return nullptr; }
+  SearchConfig cfg;
+  cfg.devices.assign(devices, devices + n_devices);
+  cfg.lanes = lanes;
+  cfg.chunks_per_batch = chunks_per_batch;
+  cfg.check_threads = check_threads;
+  khh_session* s = new khh_session();
+  std::string e;
+  if (s->s.open(t->t, cfg, e)) {
+    set_err(err, errlen, e);
+    delete s;
+    return nullptr;
+  }
+  return s;
+}
+
+void khh_session_close(khh_session* s) { delete s; }
+
+int khh_session_run(khh_session* s, const uint8_t* targets_xy, int n_targets, const uint8_t start_be[32],
+                    const uint8_t end_be[32], uint64_t max_chunks, int random_chunks, int* found, uint8_t* keys_be,
+                    uint64_t* stats_out, char* err, size_t errlen) {
+  if (!s || !targets_xy || n_targets <= 0) return KHB_EINVAL;
+  std::vector<Target> tg((size_t)n_targets);
+  for (int k = 0; k < n_targets; ++k) tg[k].p = pt_from_be(targets_xy + 64 * k);
+  SearchCallbacks cb;
+  std::vector<int> f;
+  std::vector<U256> keys;
+  SearchStats st;
+  std::string e;
+  int rc = s->s.run(tg, U256::from_be(start_be), U256::from_be(end_be), cb, f, keys, st, e, max_chunks,
+                    random_chunks != 0);
+  for (int k = 0; k < n_targets; ++k) {
+    if (found) found[k] = f.empty() ? 0 : f[k];
+    if (keys_be) (f.empty() ? U256() : keys[k]).to_be(keys_be + 32 * k);
+  }
+  if (stats_out) {
+    stats_out[0] = st.chunks;
+    stats_out[1] = st.giant_steps;
+    stats_out[2] = st.candidates;
+    stats_out[3] = st.degenerate;
+    stats_out[4] = (uint64_t)(st.kernel_seconds * 1e6);
+    stats_out[5] = st.launches;
+  }
+  if (rc) set_err(err, errlen, e);
+  return rc;
+}
+
+int khh_search(const khh_tables* t, const uint8_t* targets_xy, int n_targets, const uint8_t start_be[32],
+               const uint8_t end_be[32], const int* devices, int n_devices, uint32_t lanes,
+               uint32_t chunks_per_batch, uint64_t max_chunks, int* found, uint8_t* keys_be, uint64_t* stats_out,
+               char* err, size_t errlen) {
+  khh_session* s = khh_session_open(t, devices, n_devices, lanes, chunks_per_batch, 0, err, errlen);
+  if (!s) return KHB_ENODEV;
+  int rc = khh_session_run(s, targets_xy, n_targets, start_be, end_be, max_chunks, 0, found, keys_be, stats_out,
+                           err, errlen);
+  khh_session_close(s);
+  return rc;
+}
+
+int khh_pubkey(const uint8_t key_be[32], uint8_t out_xy[64]) {
+  const U256 k = U256::from_be(key_be);
+  if (k.is_zero() || k >= secp_order()) return KHB_EINVAL;
+  pt_to_be(out_xy, mul_g(k));
+  return 0;
+}
+
+int khh_parse_pubkey(const char* hex, uint8_t out_xy[64], int* compressed) {
+  Pt p;
+  bool c = true;
+  if (!parse_pubkey_hex(hex, p, c, nullptr)) return KHB_EINVAL;
+  pt_to_be(out_xy, p);
+  if (compressed) *compressed = c ? 1 : 0;
+  return 0;
+}
+
+}  // extern "C"

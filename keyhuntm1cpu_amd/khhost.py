@@ -1,0 +1,198 @@
+"""ctypes binding of libkhhost.so (include/khhost.h): the C++ host engine — BSGS geometry, tables,
+chunk centres, second/third check and the multi-GPU search driver the keyhunt_amd CLI runs."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import LIB_DIR
+
+LIB_PATH = os.path.join(LIB_DIR, "libkhhost.so")
+
+_lib = None
+
+
+class KhhError(RuntimeError):
+    pass
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise KhhError(f"{LIB_PATH} not built: run `make`")
+        L = C.CDLL(LIB_PATH)
+        P = C.POINTER
+        L.khh_tables_new.restype = C.c_void_p
+        L.khh_tables_new.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_uint32, C.c_char_p, C.c_size_t]
+        L.khh_tables_free.argtypes = [C.c_void_p]
+        L.khh_params.argtypes = [C.c_void_p, P(C.c_uint64)]
+        L.khh_bloom.restype = P(C.c_uint8)
+        L.khh_bloom.argtypes = [C.c_void_p, C.c_int, C.c_int, P(C.c_uint64), P(C.c_uint64), P(C.c_uint32)]
+        L.khh_giant_table.argtypes = [C.c_void_p, C.c_char_p]
+        L.khh_amp_table.argtypes = [C.c_void_p, C.c_int, C.c_char_p]
+        L.khh_lane_offsets.restype = C.c_uint32
+        L.khh_lane_offsets.argtypes = [C.c_void_p, C.c_char_p, P(C.c_uint32)]
+        L.khh_bptable.restype = P(C.c_uint8)
+        L.khh_bptable.argtypes = [C.c_void_p, P(C.c_uint64)]
+        L.khh_chunk_centre.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p]
+        L.khh_secondcheck.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_char_p, C.c_char_p]
+        L.khh_search.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, P(C.c_int), C.c_int,
+                                 C.c_uint32, C.c_uint32, C.c_uint64, P(C.c_int), C.c_char_p, P(C.c_uint64),
+                                 C.c_char_p, C.c_size_t]
+        L.khh_session_open.restype = C.c_void_p
+        L.khh_session_open.argtypes = [C.c_void_p, P(C.c_int), C.c_int, C.c_uint32, C.c_uint32, C.c_int, C.c_char_p,
+                                       C.c_size_t]
+        L.khh_session_run.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, C.c_uint64, C.c_int,
+                                      P(C.c_int), C.c_char_p, P(C.c_uint64), C.c_char_p, C.c_size_t]
+        L.khh_session_close.argtypes = [C.c_void_p]
+        L.khh_pubkey.argtypes = [C.c_char_p, C.c_char_p]
+        L.khh_parse_pubkey.argtypes = [C.c_char_p, C.c_char_p, P(C.c_int)]
+        _lib = L
+    return _lib
+
+
+def _b32(v: int) -> bytes:
+    return int(v).to_bytes(32, "big")
+
+
+def pubkey(k: int) -> bytes:
+    out = C.create_string_buffer(64)
+    if lib().khh_pubkey(_b32(k), out):
+        raise KhhError("invalid private key")
+    return out.raw
+
+
+def parse_pubkey(s: str) -> tuple[bytes, bool] | None:
+    out = C.create_string_buffer(64)
+    comp = C.c_int(0)
+    if lib().khh_parse_pubkey(s.encode(), out, C.byref(comp)):
+        return None
+    return out.raw, bool(comp.value)
+
+
+class Tables:
+    """keyhunt's BSGS tables built by the product host engine."""
+
+    def __init__(self, n: str | None = None, k: int = 1, threads: int = 0, gpl: int = 4):
+        err = C.create_string_buffer(256)
+        self.h = lib().khh_tables_new(n.encode() if n else None, k, threads, gpl, err, 256)
+        if not self.h:
+            raise KhhError(err.value.decode())
+        p = (C.c_uint64 * 10)()
+        lib().khh_params(self.h, p)
+        (self.m, self.m2, self.m3, self.aux, self.cycles, self.n_low, self.l1ext, self.items1, self.items2,
+         self.items3) = [int(v) for v in p]
+
+    def close(self) -> None:
+        if self.h:
+            lib().khh_tables_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def bloom(self, level: int, idx: int) -> tuple[bytes, int, int]:
+        nb, bits, h = C.c_uint64(), C.c_uint64(), C.c_uint32()
+        p = lib().khh_bloom(self.h, level, idx, C.byref(nb), C.byref(bits), C.byref(h))
+        return C.string_at(p, nb.value), int(bits.value), int(h.value)
+
+    def bloom_concat(self, level: int = 1) -> tuple[bytes, int, int, int]:
+        parts = [self.bloom(level, i)[0] for i in range(256)]
+        _, bits, h = self.bloom(level, 0)
+        return b"".join(parts), len(parts[0]), bits, h
+
+    def giant_table(self) -> bytes:
+        b = C.create_string_buffer(513 * 64)
+        lib().khh_giant_table(self.h, b)
+        return b.raw
+
+    def amp_table(self, level: int) -> bytes:
+        b = C.create_string_buffer(32 * 64)
+        lib().khh_amp_table(self.h, level, b)
+        return b.raw
+
+    def lane_offsets(self) -> tuple[bytes, int]:
+        g = C.c_uint32()
+        n = lib().khh_lane_offsets(self.h, None, C.byref(g))
+        b = C.create_string_buffer(64 * n)
+        lib().khh_lane_offsets(self.h, b, C.byref(g))
+        return b.raw, int(g.value)
+
+    def bptable(self) -> list[tuple[bytes, int]]:
+        n = C.c_uint64()
+        p = lib().khh_bptable(self.h, C.byref(n))
+        raw = C.string_at(p, 16 * n.value)
+        return [(raw[16 * i:16 * i + 6], int.from_bytes(raw[16 * i + 8:16 * i + 16], "little")) for i in range(n.value)]
+
+    def chunk_centre(self, base: int, target_xy: bytes) -> bytes:
+        out = C.create_string_buffer(64)
+        lib().khh_chunk_centre(self.h, _b32(base), target_xy, out)
+        return out.raw
+
+    def secondcheck(self, base: int, a: int, target_xy: bytes) -> int | None:
+        key = C.create_string_buffer(32)
+        if lib().khh_secondcheck(self.h, _b32(base), a, target_xy, key):
+            return int.from_bytes(key.raw, "big")
+        return None
+
+    def search(self, targets_xy: list[bytes], start: int, end: int, devices=(0,), lanes: int = 0,
+               chunks_per_batch: int = 0, max_chunks: int = 0):
+        n = len(targets_xy)
+        found = (C.c_int * n)()
+        keys = C.create_string_buffer(32 * n)
+        stats = (C.c_uint64 * 6)()
+        devs = (C.c_int * len(devices))(*devices)
+        err = C.create_string_buffer(256)
+        rc = lib().khh_search(self.h, b"".join(targets_xy), n, _b32(start), _b32(end), devs, len(devices), lanes,
+                              chunks_per_batch, max_chunks, found, keys, stats, err, 256)
+        if rc:
+            raise KhhError(f"search failed ({rc}): {err.value.decode()}")
+        res = [int.from_bytes(keys.raw[32 * i:32 * i + 32], "big") if found[i] else None for i in range(n)]
+        return res, {"chunks": stats[0], "giant_steps": stats[1], "candidates": stats[2], "degenerate": stats[3],
+                     "kernel_s": stats[4] / 1e6, "launches": stats[5]}
+
+
+_STAT_KEYS = ("chunks", "giant_steps", "candidates", "degenerate", "kernel_s", "launches")
+
+
+class Session:
+    """Opened devices with the tables resident in HBM (khh_session_*)."""
+
+    def __init__(self, tables: Tables, devices=(0,), lanes: int = 0, chunks_per_batch: int = 0,
+                 check_threads: int = 0):
+        self.tables = tables
+        devs = (C.c_int * len(devices))(*devices)
+        err = C.create_string_buffer(256)
+        self.h = lib().khh_session_open(tables.h, devs, len(devices), lanes, chunks_per_batch, check_threads, err, 256)
+        if not self.h:
+            raise KhhError(err.value.decode())
+
+    def close(self) -> None:
+        if self.h:
+            lib().khh_session_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def run(self, targets_xy: list[bytes], start: int, end: int, max_chunks: int = 0, random_chunks: bool = False):
+        n = len(targets_xy)
+        found = (C.c_int * n)()
+        keys = C.create_string_buffer(32 * n)
+        stats = (C.c_uint64 * 6)()
+        err = C.create_string_buffer(256)
+        rc = lib().khh_session_run(self.h, b"".join(targets_xy), n, _b32(start), _b32(end), max_chunks,
+                                   1 if random_chunks else 0, found, keys, stats, err, 256)
+        if rc:
+            raise KhhError(f"search failed ({rc}): {err.value.decode()}")
+        res = [int.from_bytes(keys.raw[32 * i:32 * i + 32], "big") if found[i] else None for i in range(n)]
+        st = {k: int(stats[i]) for i, k in enumerate(_STAT_KEYS)}
+        st["kernel_s"] = stats[4] / 1e6
+        return res, st

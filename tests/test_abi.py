@@ -1,0 +1,51 @@
+"""CPU-only checks of the native boundary: every symbol include/*.h declares is exported by the
+built libraries, and the libraries load without a GPU (no compute calls)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+from keyhuntm1cpu_amd import LIB_DIR, REPO_DIR
+
+
+def declared(header: str) -> list[str]:
+    src = open(os.path.join(REPO_DIR, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(kh[bh]_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_khbsgs_exports_every_declared_symbol():
+    lib = C.CDLL(os.path.join(LIB_DIR, "libkhbsgs.so"))
+    names = declared("khbsgs.h")
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_khhost_exports_every_declared_symbol():
+    lib = C.CDLL(os.path.join(LIB_DIR, "libkhhost.so"))
+    names = declared("khhost.h")
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_no_gpu_fails_loudly():
+    """Without a gfx950 device the library refuses to open (no CPU fallback)."""
+    from keyhuntm1cpu_amd import khbsgs
+    if khbsgs.device_count() > 0:
+        return
+    try:
+        khbsgs.Engine(0)
+    except khbsgs.KhbError as e:
+        assert "gfx950" in str(e) or "device" in str(e)
+    else:
+        raise AssertionError("Engine opened without a GPU")
+
+
+def test_strerror():
+    lib = C.CDLL(os.path.join(LIB_DIR, "libkhbsgs.so"))
+    lib.khb_strerror.restype = C.c_char_p
+    assert lib.khb_strerror(0) == b"ok"
+    assert b"gfx950" in lib.khb_strerror(-2)

@@ -1,0 +1,119 @@
+"""GPU end-to-end: the product search (libkhhost -> libkhbsgs) and the keyhunt_amd CLI against the
+reference's known answers and the oracle."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+
+import pytest
+
+from keyhuntm1cpu_amd import BIN_DIR, khhost
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+P63 = "0365ec2994b8cc0a20d40dd69edfe55ca32a54bcbbaa6b0ddcff36049301a54579"
+P125 = "0233709eb11e0d4439a729f21c2c443dedb727528229713f0065721ba8fa46f00e"
+
+
+@pytest.fixture(scope="module")
+def keys():
+    with open(os.path.join(GOLD, "puzzle_keys.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def tables_k1():
+    t = khhost.Tables(None, 1, threads=16)
+    yield t
+    t.close()
+
+
+def test_puzzle30_known_answer():
+    t = khhost.Tables("0x100000", 1, threads=8)
+    xy, _ = khhost.parse_pubkey("030d282cf2ff536d2c42f105d0b8588821a915dc3f9a05bd98bb23af67a2e92a5b")
+    res, st = t.search([xy], 1 << 29, 1 << 30)
+    assert res == [0x3D94CD64]
+
+
+@pytest.mark.parametrize("nexp", [20, 24, 28])
+def test_puzzles_multi_target(keys, nexp):
+    """All puzzles whose range fits [2^(nexp+1), 2^(nexp+8)) in one multi-target run."""
+    t = khhost.Tables(hex(1 << nexp), 1, threads=8)
+    ns = [n for n in range(nexp + 2, min(nexp + 9, 46))]
+    targets = [khhost.parse_pubkey(keys[str(n)]["pubkey"])[0] for n in ns]
+    res, st = t.search(targets, 1 << (ns[0] - 1), 1 << ns[-1])
+    assert res == [int(keys[str(n)]["key"], 16) for n in ns]
+
+
+def test_puzzle63_bsgsd_known_answer(tables_k1):
+    xy, _ = khhost.parse_pubkey(P63)
+    res, st = tables_k1.search([xy], 0x7CCE500000000000, 0x7CCE600000000000)
+    assert res == [0x7CCE5EFDACCF6808]
+
+
+def test_puzzle125_not_found(tables_k1):
+    """BSGSD.md:90-92 negative case, on a 2^47-wide slice of the same range."""
+    xy, _ = khhost.parse_pubkey(P125)
+    res, st = tables_k1.search([xy], 0x4000000000000000, 0x4000800000000000)
+    assert res == [None] and st["chunks"] == 4
+
+
+def test_full_geometry_candidates_match_oracle(tables_k1, ora):
+    """Default -n (2^44), k=1: every L1 candidate of two whole chunks (2 x 4096 groups) equals the
+    oracle's (a full-size, size-independent parity check on the real bloom)."""
+    from keyhuntm1cpu_amd.khbsgs import Engine
+    bs = ora.Bsgs(None, 1)
+    key = 0x2832ED74F2B5E35EE
+    t = ora.pubkey(key)
+    bases = [key - 123456789012, (1 << 65) + (5 << 45)]
+    with Engine(0) as e:
+        bf, nb, bits, h = tables_k1.bloom_concat(1)
+        e.load_bloom(bf, nb, bits, h)
+        e.load_giant_table(tables_k1.giant_table())
+        offs, gpl = tables_k1.lane_offsets()
+        e.load_lane_offsets(offs, gpl)
+        centres = b"".join(tables_k1.chunk_centre(b, t.be64()) for b in bases)
+        got, degen, st = e.scan(centres, 0, tables_k1.cycles)
+    assert not degen
+    for j, b in enumerate(bases):
+        ref, _, _ = bs.scan(bs.chunk_start(b, t), 0, bs.cycles)
+        assert sorted(a for jj, a in got if jj == j) == sorted(ref)
+    # the key's chunk yields the key through the host second check
+    a_hits = [a for jj, a in got if jj == 0]
+    assert any(tables_k1.secondcheck(bases[0], a, t.be64()) == key for a in a_hits)
+
+
+def _cli(args, cwd):
+    exe = os.path.join(BIN_DIR, "keyhunt_amd")
+    return subprocess.run([exe] + args, cwd=cwd, capture_output=True, text=True, timeout=300)
+
+
+def test_cli_puzzle63(tmp_path):
+    (tmp_path / "63.pub").write_text(P63 + "\n\n")
+    r = _cli(["-m", "bsgs", "-f", "63.pub", "-r", "7cce500000000000:7cce600000000000", "-q", "-s", "0"], tmp_path)
+    assert r.returncode == 1, r.stdout + r.stderr          # keyhunt exits 1 after "All points were found"
+    assert "[+] Thread Key found privkey 7cce5efdaccf6808" in r.stdout
+    assert "[+] Publickey " + P63 in r.stdout
+    assert "All points were found" in r.stdout
+    kf = (tmp_path / "KEYFOUNDKEYFOUND.txt").read_text()
+    assert kf == f"Key found privkey 7cce5efdaccf6808\nPublickey {P63}\n"
+
+
+def test_cli_multi_target_bits(tmp_path, keys):
+    lines = [keys[str(n)]["pubkey"] + " # puzzle " + str(n) for n in (31, 32, 33)]
+    lines.append("04" + "zz" * 64)                          # invalid line: reported, skipped
+    (tmp_path / "t.txt").write_text("\n".join(lines) + "\n")
+    r = _cli(["-m", "bsgs", "-f", "t.txt", "-b", "33", "-n", "0x1000000", "-q", "-s", "0"], tmp_path)
+    # puzzles 31/32 lie below 2^32: only 33 is in -b 33's range
+    assert "privkey " + keys["33"]["key"] in r.stdout
+    assert r.returncode == 0 and "End" in r.stdout
+
+
+def test_cli_rejects_bad_geometry(tmp_path):
+    (tmp_path / "63.pub").write_text(P63 + "\n")
+    r = _cli(["-m", "bsgs", "-f", "63.pub", "-b", "63", "-n", "0x10000"], tmp_path)    # M = 256
+    assert r.returncode == 1 and "M value is not divisible by 1024" in r.stderr
+    (tmp_path / "66.txt").write_text("13zb1hQbWVsc2S7ZTZnP2G4undNNpdh5so\n")
+    r = _cli(["-m", "bsgs", "-f", "66.txt", "-b", "66"], tmp_path)
+    assert r.returncode == 1 and "There is no valid data in the file" in r.stderr

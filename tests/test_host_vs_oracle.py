@@ -1,0 +1,89 @@
+"""CPU parity: the product host engine (libkhhost.so) against the oracle restatement.
+
+Everything the host builds feeds the GPU, so it must be bit-exact: geometry, all three bloom
+levels, bPtable, the giant tables, chunk centres and second/third-check outcomes.
+"""
+from __future__ import annotations
+
+import random
+
+import pytest
+
+from keyhuntm1cpu_amd import khhost
+
+GEOMS = [("0x100000", 1), ("0x100000000", 1), ("0x100000000", 3), ("0x10000000000", 2)]
+
+
+@pytest.fixture(scope="module", params=GEOMS, ids=[f"{n}-k{k}" for n, k in GEOMS])
+def pair(request, ora):
+    n, k = request.param
+    h = khhost.Tables(n, k, threads=8, gpl=4)
+    o = ora.Bsgs(n, k, threads=8)
+    yield h, o
+    h.close()
+    o.close()
+
+
+def test_geometry(pair):
+    h, o = pair
+    assert (h.m, h.m2, h.m3, h.aux, h.cycles, h.n_low, h.l1ext, h.items1, h.items2, h.items3) == \
+           (o.m, o.m2, o.m3, o.aux, o.cycles, o.n_low, o.l1ext, o.items1, o.items2, o.items3)
+
+
+@pytest.mark.parametrize("level", [1, 2, 3])
+def test_blooms_bit_exact(pair, level):
+    h, o = pair
+    bh = h.bloom_concat(level)
+    bo = o.bloom_concat(level)
+    assert bh[1:] == bo[1:]
+    assert bh[0] == bo[0]
+
+
+def test_giant_and_amp_tables(pair):
+    h, o = pair
+    assert h.giant_table() == o.giant_table()
+    assert h.amp_table(2) == o.amp_table(2)
+    assert h.amp_table(3) == o.amp_table(3)
+
+
+def test_bptable(pair):
+    h, o = pair
+    assert h.bptable() == o.bptable()
+
+
+def test_lane_offsets(pair, ora):
+    h, o = pair
+    offs, gpl = h.lane_offsets()
+    assert gpl == 4 and len(offs) == 64 * ((o.cycles + 3) // 4)
+    for m in range(1, len(offs) // 64):
+        exp = ora.negation(ora.pubkey(m * gpl * 2048 * o.m)).be64()
+        assert offs[64 * m:64 * m + 64] == exp
+
+
+def test_chunk_centres_and_secondcheck(pair, ora):
+    h, o = pair
+    rng = random.Random(7)
+    for _ in range(6):
+        key = rng.randrange(1 << 60, 1 << 62)
+        base = key - rng.randrange(1, 2 * o.n_low * 2)        # key within ~2 chunks of base
+        base = max(base, 1)
+        t = ora.pubkey(key)
+        cen = h.chunk_centre(base, t.be64())
+        assert cen == o.chunk_start(base, t).be64()
+        cands, _, _ = o.scan(o.chunk_start(base, t), 0, min(o.cycles, 8))
+        for a in cands[:20]:
+            assert h.secondcheck(base, a, t.be64()) == o.secondcheck(base, a, t)
+
+
+def test_pubkey_and_parse(ora):
+    rng = random.Random(3)
+    for _ in range(50):
+        k = rng.randrange(1, ora.ORDER)
+        assert khhost.pubkey(k) == ora.pubkey(k).be64()
+        for comp in (True, False):
+            s = ora.pubkey_hex(k, comp)
+            xy, c = khhost.parse_pubkey(s)
+            assert xy == ora.pubkey(k).be64() and c == comp
+    assert khhost.parse_pubkey("02" + "00" * 31 + "05") is None or True   # may or may not be on curve
+    assert khhost.parse_pubkey("05" + "11" * 32) is None
+    assert khhost.parse_pubkey("02" + "11" * 31) is None
