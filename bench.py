@@ -28,8 +28,8 @@ sys.path.insert(0, REPO)
 MUL_OPS, SQR_OPS = 72, 44
 OPS_PER_STEP = (2561 * MUL_OPS + 1023 * SQR_OPS + 255 * SQR_OPS + 15 * MUL_OPS) / 1024.0 + 2 * 66 + 2 * 4
 # Peak of the binding unit: v_mad_u64_u32 issue rate measured on MI355X by
-# tools/microbench/intops.hip (profiles/r01_intops.txt).
-PEAK_MULOPS_T = float(os.environ.get("KHB_PEAK_MULOPS_T", "29.96"))
+# tools/microbench/intops2.hip at full occupancy (profiles/r01_intops2.txt).
+PEAK_MULOPS_T = float(os.environ.get("KHB_PEAK_MULOPS_T", "32.04"))
 HBM_PEAK_GBS = 8000.0
 
 PUZZLE66_KEY = 0x2832ED74F2B5E35EE            # public solution; pinned to tests/66.rmd below
@@ -77,6 +77,7 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from keyhuntm1cpu_amd import khhost
+    from keyhuntm1cpu_amd.partition import rank_range
     host_threads = min(16, os.cpu_count() or 1)
     t0 = time.time()
     tables = khhost.Tables(None, args.k, threads=host_threads, gpl=4)
@@ -84,10 +85,7 @@ def main():
     target = puzzle66_target()
     two_n = 2 * (tables.n_low)                     # 2N keys per chunk
     lo, hi = 1 << 65, 1 << 66                      # -b 66
-    n_chunks = (hi - lo + two_n - 1) // two_n
-    per = n_chunks // world
-    start = lo + rank * per * two_n
-    end = start + per * two_n
+    start, end = rank_range(lo, hi, two_n, rank, world)
     sess = khhost.Session(tables, devices=[local], chunks_per_batch=args.chunks, check_threads=host_threads)
 
     def sync():
