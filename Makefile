@@ -43,3 +43,29 @@ clean:
 	rm -rf $(LIBDIR) $(BINDIR) build oracle/build
 
 .PHONY: all oracle clean
+
+# Kernel variants for A/B timing (tools/perf_variants.py); not used by the product.
+VARIANTS := w2 w4
+variants: $(patsubst %,$(LIBDIR)/variants/libkhbsgs_%.so,$(VARIANTS))
+$(LIBDIR)/variants/libkhbsgs_w%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_WAVES_PER_SIMD=$* -shared -o $@ $(CSRC)/khbsgs.hip
+$(LIBDIR)/variants/libkhbsgs_r%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_PROBE_BITS=$* -shared -o $@ $(CSRC)/khbsgs.hip
+$(LIBDIR)/variants/libkhbsgs_m0s%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_MUL_IMPL=0 -DKHB_SQR_IMPL=$* -shared -o $@ $(CSRC)/khbsgs.hip
+$(LIBDIR)/variants/libkhbsgs_m1s%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_MUL_IMPL=1 -DKHB_SQR_IMPL=$* -shared -o $@ $(CSRC)/khbsgs.hip
+$(LIBDIR)/variants/libkhbsgs_m2s%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_MUL_IMPL=2 -DKHB_SQR_IMPL=$* -shared -o $@ $(CSRC)/khbsgs.hip
+$(LIBDIR)/variants/libkhbsgs_d%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_DRAIN_WIDTH=$* -DKHB_PROBE_BITS=1 -shared -o $@ $(CSRC)/khbsgs.hip
+$(LIBDIR)/variants/libkhbsgs_p%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_PROBE_MODE=$* -shared -o $@ $(CSRC)/khbsgs.hip
+.PHONY: variants

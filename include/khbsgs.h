@@ -63,13 +63,16 @@ typedef struct {
 
 /* ---- device / context ---- */
 int khb_device_count(int* n);
-/* lanes: persistent-grid size in work lanes (0 = auto: 8 waves per CU).  Sizes the scratch. */
+/* lanes: persistent-grid size in work lanes (0 = auto: one full residency of the kernel,
+ * CUs x 4 SIMDs x waves-per-SIMD x 64).  Sizes the scratch. */
 int khb_open(int device, uint32_t lanes, khb_ctx** out);
 int khb_close(khb_ctx* ctx);
 const char* khb_strerror(int code);
 int khb_last_hip_error(const khb_ctx* ctx);
 /* The hipStream_t the context launches on (for external HIP events / synchronisation). */
 void* khb_stream(khb_ctx* ctx);
+/* Persistent-grid size of the context in work lanes (one lane = groups_per_lane groups at a time). */
+uint32_t khb_lanes(const khb_ctx* ctx);
 
 /* ---- tables (bsgs setup, keyhunt.cpp:1185-1364) ---- */
 /* Level-1 bloom: 256 sub-blooms of identical geometry concatenated in sub-bloom order

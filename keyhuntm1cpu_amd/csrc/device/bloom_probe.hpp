@@ -3,9 +3,10 @@
 // (Int::Get32Bytes of x, keyhunt.cpp:3945-3946).
 //
 // The probe is split so the GPU pays only for what a miss needs: bit 0 of a probe is
-// (a mod bits) and depends on the first hash alone, so the second XXH64 runs only for the ~50 %
-// of points whose first bit is set; later bit positions (a + b*i) mod bits are stepped
-// incrementally (64-bit wrap tracked by the carry, corrected by 2^64 mod bits).
+// (a mod bits) and depends on the first hash alone, so the second XXH64 (bloom_rest) runs only
+// for the ~50 % of points whose first bit is set — the scan kernel queues those survivors and
+// finishes them in full waves; later bit positions (a + b*i) mod bits are stepped incrementally
+// (64-bit wrap tracked by the carry, corrected by 2^64 mod bits).
 #pragma once
 #include <stdint.h>
 #include "fe.hpp"
@@ -85,27 +86,81 @@ KHB_HD uint64_t mod_bits(uint64_t h, const BloomGeom& g) {
 
 KHB_HD bool test_bit(const uint8_t* bf, uint64_t bit) { return (bf[bit >> 3] >> (bit & 7)) & 1u; }
 
-// bloom_check(&bloom_bP[xb[0]], xb, 32) != 0 for x; bf_all = 256 concatenated sub-blooms.
-KHB_HD bool bloom_probe_x(const uint8_t* __restrict__ bf_all, const BloomGeom& g, const Fe& x) {
-  const uint8_t* bf = bf_all + (uint64_t)(x.v[7] >> 24) * g.bytes_per_sub;
-  uint64_t w[4];
-  x_words(w, x);
-  uint64_t a = xxh64_32(w, KHB_BLOOM_SEED);
+// The sub-bloom bloom_bP[xb[0]] of x (keyhunt.cpp:3946-3947); bf_all = 256 concatenated sub-blooms.
+KHB_HD const uint8_t* sub_bloom(const uint8_t* __restrict__ bf_all, const BloomGeom& g, const Fe& x) {
+  return bf_all + (uint64_t)(x.v[7] >> 24) * g.bytes_per_sub;
+}
+
+// Hashes 1..hashes-1 of bloom_check (bloom.cpp:141-150) for an x whose first hash `a` already hit:
+// b = XXH64(x, seed = a), bit i at (a + b*i) mod bits.  R bit positions are fetched per round
+// (independent loads, one memory round trip); the result is the same AND of all bits for any R.
+template <int R>
+KHB_HD bool bloom_rest_r(const uint8_t* __restrict__ bf, const BloomGeom& g, const uint64_t w[4], uint64_t a) {
   uint64_t pos = mod_bits(a, g);
-  if (!test_bit(bf, pos)) return false;
-  uint64_t b = xxh64_32(w, a);
-  uint64_t bm = mod_bits(b, g);
+  const uint64_t b = xxh64_32(w, a);
+  const uint64_t bm = mod_bits(b, g);
   uint64_t h = a;
-  for (uint32_t i = 1; i < g.hashes; ++i) {
-    uint64_t nh = h + b;
-    bool wrapped = nh < h;
-    h = nh;
-    pos += bm;
-    if (pos >= g.bits) pos -= g.bits;
-    if (wrapped) pos = (pos >= g.wrap) ? pos - g.wrap : pos + g.bits - g.wrap;
-    if (!test_bit(bf, pos)) return false;
+  for (uint32_t i = 1; i < g.hashes; i += R) {
+    uint64_t ps[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint64_t nh = h + b;
+      const bool wrapped = nh < h;
+      h = nh;
+      pos += bm;
+      if (pos >= g.bits) pos -= g.bits;
+      if (wrapped) pos = (pos >= g.wrap) ? pos - g.wrap : pos + g.bits - g.wrap;
+      ps[r] = pos;
+    }
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < R; ++r) ok &= (i + r >= g.hashes) || test_bit(bf, ps[r]);
+    if (!ok) return false;
   }
   return true;
+}
+
+// bloom_rest for two independent x at once (ok1/ok2 in: entry valid, out: all bits set).  Each
+// round fetches the next bit of both live entries, so one memory round trip serves both.
+KHB_HD void bloom_rest_pair(const BloomGeom& g, const uint8_t* __restrict__ bf1, const uint64_t w1[4], uint64_t a1,
+                            bool& ok1, const uint8_t* __restrict__ bf2, const uint64_t w2[4], uint64_t a2,
+                            bool& ok2) {
+  uint64_t pos1 = mod_bits(a1, g), pos2 = mod_bits(a2, g);
+  const uint64_t b1 = xxh64_32(w1, a1), b2 = xxh64_32(w2, a2);
+  const uint64_t bm1 = mod_bits(b1, g), bm2 = mod_bits(b2, g);
+  uint64_t h1 = a1, h2 = a2;
+  for (uint32_t i = 1; i < g.hashes && (ok1 || ok2); ++i) {
+    uint64_t nh = h1 + b1;
+    bool wrapped = nh < h1;
+    h1 = nh;
+    pos1 += bm1;
+    if (pos1 >= g.bits) pos1 -= g.bits;
+    if (wrapped) pos1 = (pos1 >= g.wrap) ? pos1 - g.wrap : pos1 + g.bits - g.wrap;
+    nh = h2 + b2;
+    wrapped = nh < h2;
+    h2 = nh;
+    pos2 += bm2;
+    if (pos2 >= g.bits) pos2 -= g.bits;
+    if (wrapped) pos2 = (pos2 >= g.wrap) ? pos2 - g.wrap : pos2 + g.bits - g.wrap;
+    const uint32_t t1 = ok1 ? bf1[pos1 >> 3] : 0u;
+    const uint32_t t2 = ok2 ? bf2[pos2 >> 3] : 0u;
+    ok1 = ok1 && ((t1 >> (pos1 & 7)) & 1u);
+    ok2 = ok2 && ((t2 >> (pos2 & 7)) & 1u);
+  }
+}
+
+KHB_HD bool bloom_rest(const uint8_t* __restrict__ bf, const BloomGeom& g, const uint64_t w[4], uint64_t a) {
+  return bloom_rest_r<1>(bf, g, w, a);
+}
+
+// bloom_check(&bloom_bP[xb[0]], xb, 32) != 0 for x (bloom.cpp:128-156).
+KHB_HD bool bloom_probe_x(const uint8_t* __restrict__ bf_all, const BloomGeom& g, const Fe& x) {
+  const uint8_t* bf = sub_bloom(bf_all, g, x);
+  uint64_t w[4];
+  x_words(w, x);
+  const uint64_t a = xxh64_32(w, KHB_BLOOM_SEED);
+  if (!test_bit(bf, mod_bits(a, g))) return false;
+  return bloom_rest(bf, g, w, a);
 }
 
 }  // namespace khb

@@ -1,0 +1,692 @@
+// gfx950 fast path for the secp256k1 field: hand-placed carry chains.
+//
+// Why: the scan kernel is VALU-issue-bound (profiles/r01_pmc.txt).  The portable fe.hpp compiles
+// to 390 VALU instructions per multiply — 216 of them v_mov_b32 materialising zero-extended
+// 64-bit addends.  Here each 32x32 partial product is one v_mad_u64_u32 whose carry-out (VCC)
+// is absorbed by one VOP2 v_addc_co_u32 (product scanning), and add/sub are single carry chains.
+//
+// gfx950 hazard: a VALU that writes VCC (v_add_co/v_sub_co/v_mad_u64_u32 carry-out) needs one
+// wait state before a VALU reads that VCC as carry-in — hipcc pads its own chains with `s_nop 0`
+// (seen in its ISA for __builtin_addc), but nothing inside an asm string is padded
+// (cdna_hip_programming.md §5.7 item 2), so every carry consumer below is preceded by `s_nop 0`.
+//
+// Value contract (checked by tests/test_gpu_scan.py::test_field_ops and every x-dump test):
+//   * fm_mul / fm_sqr return a value < 2^256 congruent to a*b mod p, not necessarily < p ("lazy").
+//   * fm_sub(a, b) is correct for a < 2^256 and b < p; its result is < 2^256 (< p if it borrowed).
+//   * fm_add(a, b) needs a, b < p and returns a canonical value.
+//   * fm_canon brings any value < 2^256 into [0, p).  Values that are hashed, compared or used as a
+//     subtrahend (x-coordinates, centres) are canonicalised, so every observable equals the
+//     reference's canonical Int (IntMod.cpp) bit for bit.
+#pragma once
+#include <stdint.h>
+
+#include "fe.hpp"
+
+namespace khb {
+
+#define FM_DEV __device__ __forceinline__
+
+// acc += a*b ; c2 += carry-out
+FM_DEV void fm_madc(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(c2)
+      : "v"(a), "v"(b)
+      : "vcc");
+}
+
+template <int K>
+FM_DEV void fm_col(uint64_t& acc, uint32_t& c2, const uint32_t* a, const uint32_t* b) {
+#pragma unroll
+  for (int i = (K > 7 ? K - 7 : 0); i <= (K < 7 ? K : 7); ++i) fm_madc(acc, c2, a[i], b[K - i]);
+}
+
+// 512-bit product, product scanning (column k = sum of a_i*b_{k-i}).
+FM_DEV void fm_mul512(uint32_t t[16], const uint32_t* a, const uint32_t* b) {
+  uint64_t acc = (uint64_t)a[0] * b[0];
+  t[0] = (uint32_t)acc;
+  acc >>= 32;
+  uint32_t c2 = 0;
+#define FM_COL(K)                                      \
+  fm_col<K>(acc, c2, a, b);                            \
+  t[K] = (uint32_t)acc;                                \
+  acc = (acc >> 32) | ((uint64_t)c2 << 32);            \
+  c2 = 0;
+  FM_COL(1) FM_COL(2) FM_COL(3) FM_COL(4) FM_COL(5) FM_COL(6) FM_COL(7)
+  FM_COL(8) FM_COL(9) FM_COL(10) FM_COL(11) FM_COL(12) FM_COL(13) FM_COL(14)
+#undef FM_COL
+  t[15] = (uint32_t)acc;
+}
+
+// ---- 512-bit products without accumulator shuffling ----------------------------------------
+// Column k (sum of a_i*b_{k-i}) accumulates in its own 64-bit pair A[k]; the carries out of A[k]
+// (weight 2^(32k+64)) are counted in cw[k] and seed A[k+2], which they align with exactly.  So no
+// register is ever moved between columns; one add chain at the end folds hi(A[k-1]) into word k:
+//   sum_k A[k] 2^(32k) (+ cw[13] 2^480) == a*b.
+// The first product of a column cannot overflow (seed < 2^4), the others carry into cw[k].
+
+// acc += a*b; cw = carry-out (first carry of a column: no zero-initialisation needed)
+FM_DEV void fm_madc_first(uint64_t& acc, uint32_t& cw, uint32_t a, uint32_t b) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %4, vcc"
+      : "+v"(acc), "=v"(cw)
+      : "v"(a), "v"(b), "v"(0u)
+      : "vcc");
+}
+
+// Column K of a*b (generic product): A seeded, cw receives its carries.
+template <int K>
+FM_DEV void fm_colx(uint64_t& A, uint32_t& cw, const uint32_t* a, const uint32_t* b) {
+  constexpr int lo = K > 7 ? K - 7 : 0, hi = K < 7 ? K : 7;
+  A += (uint64_t)a[lo] * b[K - lo];
+  if constexpr (hi > lo) {
+    fm_madc_first(A, cw, a[lo + 1], b[K - lo - 1]);
+#pragma unroll
+    for (int i = lo + 2; i <= hi; ++i) fm_madc(A, cw, a[i], b[K - i]);
+  }
+}
+
+// t[k] = lo(A[k]) + hi(A[k-1]) + carry, k = 1..14; t[15] = cw13 + hi(A[14]) + carry.
+FM_DEV void fm_fold_cols(uint32_t t[16], const uint64_t A[15], uint32_t cw13) {
+#define FM_LO(k) "v"((uint32_t)A[k])
+#define FM_HI(k) "v"((uint32_t)(A[k] >> 32))
+  t[0] = (uint32_t)A[0];
+  asm("v_add_co_u32_e32 %0, vcc, %15, %16\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %17, %18, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %19, %20, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %21, %22, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %23, %24, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %25, %26, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %27, %28, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %29, %30, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %8, vcc, %31, %32, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %9, vcc, %33, %34, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %10, vcc, %35, %36, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %11, vcc, %37, %38, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %12, vcc, %39, %40, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %13, vcc, %41, %42, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %14, vcc, %43, %44, vcc"
+      : "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7]),
+        "=&v"(t[8]), "=&v"(t[9]), "=&v"(t[10]), "=&v"(t[11]), "=&v"(t[12]), "=&v"(t[13]), "=&v"(t[14]),
+        "=&v"(t[15])
+      : FM_LO(1), FM_HI(0), FM_LO(2), FM_HI(1), FM_LO(3), FM_HI(2), FM_LO(4), FM_HI(3), FM_LO(5), FM_HI(4),
+        FM_LO(6), FM_HI(5), FM_LO(7), FM_HI(6), FM_LO(8), FM_HI(7), FM_LO(9), FM_HI(8), FM_LO(10), FM_HI(9),
+        FM_LO(11), FM_HI(10), FM_LO(12), FM_HI(11), FM_LO(13), FM_HI(12), FM_LO(14), FM_HI(13), "v"(cw13),
+        FM_HI(14)
+      : "vcc");
+#undef FM_LO
+#undef FM_HI
+}
+
+FM_DEV void fm_mul512x(uint32_t t[16], const uint32_t* a, const uint32_t* b) {
+  uint64_t A[15];
+  uint32_t cw[14];
+  A[0] = (uint64_t)a[0] * b[0];
+  A[1] = 0;
+  fm_colx<1>(A[1], cw[1], a, b);
+  A[2] = 0;
+  fm_colx<2>(A[2], cw[2], a, b);
+#define FM_COLX(K)            \
+  A[K] = (uint64_t)cw[K - 2]; \
+  fm_colx<K>(A[K], cw[K], a, b);
+  FM_COLX(3) FM_COLX(4) FM_COLX(5) FM_COLX(6) FM_COLX(7) FM_COLX(8) FM_COLX(9) FM_COLX(10)
+  FM_COLX(11) FM_COLX(12) FM_COLX(13)
+#undef FM_COLX
+  A[14] = (uint64_t)cw[12];
+  A[14] += (uint64_t)a[7] * b[7];
+  fm_fold_cols(t, A, cw[13]);
+}
+
+// t_k = lo(cur) + hi(prev); the carry c_k joins cw (the carries of column k-1) as the seed of
+// column k+1, which has the same weight.  seed <= 8, so seeding never overflows a column.
+FM_DEV void fm_fold_step(uint32_t& t, uint32_t& seed, uint64_t cur, uint64_t prev, uint32_t cw) {
+  asm("v_add_co_u32_e32 %0, vcc, %2, %3\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %4, vcc"
+      : "=&v"(t), "=v"(seed)
+      : "v"((uint32_t)cur), "v"((uint32_t)(prev >> 32)), "v"(cw)
+      : "vcc");
+}
+
+// 512-bit product, seeded columns folded as they complete: only two column accumulators are
+// ever live (the all-columns-then-fold form above needs 15 pairs at its peak).
+FM_DEV void fm_mul512p(uint32_t t[16], const uint32_t* a, const uint32_t* b) {
+  uint32_t cw[14], seed;
+  uint64_t prev = (uint64_t)a[0] * b[0], cur;
+  t[0] = (uint32_t)prev;
+  cur = 0;
+  fm_colx<1>(cur, cw[1], a, b);
+  fm_fold_step(t[1], seed, cur, prev, 0u);
+  prev = cur;
+#define FM_COLP(K)                                 \
+  cur = (uint64_t)seed;                            \
+  fm_colx<K>(cur, cw[K], a, b);                    \
+  fm_fold_step(t[K], seed, cur, prev, cw[K - 1]);  \
+  prev = cur;
+  FM_COLP(2) FM_COLP(3) FM_COLP(4) FM_COLP(5) FM_COLP(6) FM_COLP(7) FM_COLP(8) FM_COLP(9) FM_COLP(10)
+  FM_COLP(11) FM_COLP(12) FM_COLP(13)
+#undef FM_COLP
+  // column 14: one product, no carry; t15 = hi(A14) + cw13 + c14
+  cur = (uint64_t)seed;
+  cur += (uint64_t)a[7] * b[7];
+  asm("v_add_co_u32_e32 %0, vcc, %2, %3\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %4, %5, vcc"
+      : "=&v"(t[14]), "=v"(t[15])
+      : "v"((uint32_t)cur), "v"((uint32_t)(prev >> 32)), "v"(cw[13]), "v"((uint32_t)(cur >> 32))
+      : "vcc");
+}
+
+// Column K of the cross sum sum_{i<j} a_i a_j 2^(32(i+j)).
+template <int K>
+FM_DEV void fm_colsq(uint64_t& A, uint32_t& cw, const uint32_t* a) {
+  constexpr int lo = K > 7 ? K - 7 : 0, hi = (K - 1) / 2;   // pairs (i, K-i), i < K-i
+  A += (uint64_t)a[lo] * a[K - lo];
+  if constexpr (hi > lo) {
+    fm_madc_first(A, cw, a[lo + 1], a[K - lo - 1]);
+#pragma unroll
+    for (int i = lo + 2; i <= hi; ++i) fm_madc(A, cw, a[i], a[K - i]);
+  }
+}
+
+// t_k = d_k + 2 c_k, word 1 (starts both carry chains): u = d + c -> carry sU; t = u + c -> sT.
+// The chains run across columns whose products use VCC, so their carries live in SGPR pairs
+// (VOP3 forms).
+FM_DEV void fm_sq_word_first(uint32_t& t, uint64_t& sU, uint64_t& sT, uint32_t d, uint32_t c) {
+  uint32_t u;
+  asm("v_add_co_u32_e64 %0, %2, %4, %5\n\t"
+      "v_add_co_u32_e64 %1, %3, %0, %5"
+      : "=&v"(u), "=v"(t), "=&s"(sU), "=&s"(sT)
+      : "v"(d), "v"(c));
+}
+FM_DEV void fm_sq_word(uint32_t& t, uint64_t& sU, uint64_t& sT, uint32_t d, uint32_t c) {
+  uint32_t u;
+  asm("s_nop 0\n\t"
+      "v_addc_co_u32_e64 %0, %2, %4, %5, %2\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e64 %1, %3, %0, %5, %3"
+      : "=&v"(u), "=v"(t), "+s"(sU), "+s"(sT)
+      : "v"(d), "v"(c));
+}
+
+// a^2 progressively: cross-sum words c_k are folded as their columns complete and immediately
+// combined with the diagonal words d_k; peak liveness is the 16 output words plus a handful.
+FM_DEV void fm_sqr512p(uint32_t t[16], const uint32_t* a) {
+  uint32_t cw[14], seed, c;
+  uint64_t prev, cur, sU, sT, D;
+  D = (uint64_t)a[0] * a[0];
+  t[0] = (uint32_t)D;
+  // column 1: a0*a1
+  cur = (uint64_t)a[0] * a[1];
+  c = (uint32_t)cur;
+  seed = 0;
+  fm_sq_word_first(t[1], sU, sT, (uint32_t)(D >> 32), c);
+  prev = cur;
+  // column 2: a0*a2 (single product; the fold of word 2 creates the first seed)
+  cur = (uint64_t)a[0] * a[2];
+  fm_fold_step(c, seed, cur, prev, 0u);
+  D = (uint64_t)a[1] * a[1];
+  fm_sq_word(t[2], sU, sT, (uint32_t)D, c);
+  prev = cur;
+#define FM_SQP(K, CWPREV, DWORD)                   \
+  cur = (uint64_t)seed;                            \
+  fm_colsq<K>(cur, cw[K], a);                      \
+  fm_fold_step(c, seed, cur, prev, CWPREV);        \
+  fm_sq_word(t[K], sU, sT, DWORD, c);              \
+  prev = cur;
+  FM_SQP(3, 0u, (uint32_t)(D >> 32))
+  D = (uint64_t)a[2] * a[2];
+  FM_SQP(4, cw[3], (uint32_t)D)
+  FM_SQP(5, cw[4], (uint32_t)(D >> 32))
+  D = (uint64_t)a[3] * a[3];
+  FM_SQP(6, cw[5], (uint32_t)D)
+  FM_SQP(7, cw[6], (uint32_t)(D >> 32))
+  D = (uint64_t)a[4] * a[4];
+  FM_SQP(8, cw[7], (uint32_t)D)
+  FM_SQP(9, cw[8], (uint32_t)(D >> 32))
+  D = (uint64_t)a[5] * a[5];
+  FM_SQP(10, cw[9], (uint32_t)D)
+  FM_SQP(11, cw[10], (uint32_t)(D >> 32))
+  D = (uint64_t)a[6] * a[6];
+#undef FM_SQP
+  // columns 12, 13: single products (5,7), (6,7): no cw of their own
+  cur = (uint64_t)seed;
+  cur += (uint64_t)a[5] * a[7];
+  fm_fold_step(c, seed, cur, prev, cw[11]);
+  fm_sq_word(t[12], sU, sT, (uint32_t)D, c);
+  prev = cur;
+  cur = (uint64_t)seed;
+  cur += (uint64_t)a[6] * a[7];
+  fm_fold_step(c, seed, cur, prev, 0u);
+  fm_sq_word(t[13], sU, sT, (uint32_t)(D >> 32), c);
+  prev = cur;
+  // column 14 holds no cross product: c14 = seed + hi(A13); c15 = its carry
+  D = (uint64_t)a[7] * a[7];
+  cur = (uint64_t)seed;
+  fm_fold_step(c, seed, cur, prev, 0u);
+  fm_sq_word(t[14], sU, sT, (uint32_t)D, c);
+  fm_sq_word(t[15], sU, sT, (uint32_t)(D >> 32), seed);
+}
+
+// a^2 = 2*cross + diag: 36 products instead of 64.
+FM_DEV void fm_sqr512x(uint32_t t[16], const uint32_t* a) {
+  uint64_t A[15];
+  uint32_t cw[14];
+  A[0] = 0;
+  A[1] = 0;
+  fm_colsq<1>(A[1], cw[1], a);
+  A[2] = 0;
+  fm_colsq<2>(A[2], cw[2], a);
+  A[3] = 0;
+  fm_colsq<3>(A[3], cw[3], a);
+  A[4] = 0;
+  fm_colsq<4>(A[4], cw[4], a);
+#define FM_COLSQ(K)           \
+  A[K] = (uint64_t)cw[K - 2]; \
+  fm_colsq<K>(A[K], cw[K], a);
+  FM_COLSQ(5) FM_COLSQ(6) FM_COLSQ(7) FM_COLSQ(8) FM_COLSQ(9) FM_COLSQ(10) FM_COLSQ(11) FM_COLSQ(12)
+  FM_COLSQ(13)
+#undef FM_COLSQ
+  A[14] = 0;                  // column 14 holds no cross product (7,7 is diagonal)
+  // Only columns 3..11 hold two or more cross products, so only cw[3..11] exist; they seed
+  // A[5..13].  Columns 1, 2, 12, 13 carry nothing.
+  uint32_t c[16];
+  fm_fold_cols(c, A, 0u);     // c = cross sum (c[0] = 0)
+  uint64_t D[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) D[i] = (uint64_t)a[i] * a[i];
+  // t = D + c + c
+  uint32_t u[16];
+  asm("v_add_co_u32_e32 %0, vcc, %16, %32\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %17, %33, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %18, %34, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %19, %35, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %20, %36, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %21, %37, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %22, %38, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %23, %39, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %8, vcc, %24, %40, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %9, vcc, %25, %41, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %10, vcc, %26, %42, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %11, vcc, %27, %43, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %12, vcc, %28, %44, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %13, vcc, %29, %45, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %14, vcc, %30, %46, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %15, vcc, %31, %47, vcc"
+      : "=&v"(u[0]), "=&v"(u[1]), "=&v"(u[2]), "=&v"(u[3]), "=&v"(u[4]), "=&v"(u[5]), "=&v"(u[6]), "=&v"(u[7]),
+        "=&v"(u[8]), "=&v"(u[9]), "=&v"(u[10]), "=&v"(u[11]), "=&v"(u[12]), "=&v"(u[13]), "=&v"(u[14]),
+        "=&v"(u[15])
+      : "v"((uint32_t)D[0]), "v"((uint32_t)(D[0] >> 32)), "v"((uint32_t)D[1]), "v"((uint32_t)(D[1] >> 32)),
+        "v"((uint32_t)D[2]), "v"((uint32_t)(D[2] >> 32)), "v"((uint32_t)D[3]), "v"((uint32_t)(D[3] >> 32)),
+        "v"((uint32_t)D[4]), "v"((uint32_t)(D[4] >> 32)), "v"((uint32_t)D[5]), "v"((uint32_t)(D[5] >> 32)),
+        "v"((uint32_t)D[6]), "v"((uint32_t)(D[6] >> 32)), "v"((uint32_t)D[7]), "v"((uint32_t)(D[7] >> 32)),
+        "v"(0u), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]), "v"(c[8]), "v"(c[9]),
+        "v"(c[10]), "v"(c[11]), "v"(c[12]), "v"(c[13]), "v"(c[14]), "v"(c[15])
+      : "vcc");
+  asm("v_add_co_u32_e32 %0, vcc, %0, %16\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %1, %17, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %2, %18, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %3, %19, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %4, %20, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %5, %21, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %6, %22, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %7, %23, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %8, vcc, %8, %24, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %9, vcc, %9, %25, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %10, vcc, %10, %26, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %11, vcc, %11, %27, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %12, vcc, %12, %28, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %13, vcc, %13, %29, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %14, vcc, %14, %30, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %15, vcc, %15, %31, vcc"
+      : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]),
+        "+v"(u[8]), "+v"(u[9]), "+v"(u[10]), "+v"(u[11]), "+v"(u[12]), "+v"(u[13]), "+v"(u[14]), "+v"(u[15])
+      : "v"(0u), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]), "v"(c[8]), "v"(c[9]),
+        "v"(c[10]), "v"(c[11]), "v"(c[12]), "v"(c[13]), "v"(c[14]), "v"(c[15])
+      : "vcc");
+#pragma unroll
+  for (int i = 0; i < 16; ++i) t[i] = u[i];
+}
+
+// Reduce t (512 bits) mod p to a value < 2^256 (lazy).  2^256 = 2^32 + 977 (mod p).
+FM_DEV void fm_reduce(Fe& r, const uint32_t t[16]) {
+  const uint32_t* L = t;
+  const uint32_t* H = t + 8;
+  // T = L + (H << 32): 9 limbs + T9 (both operands near p make L + H*2^32 reach 2^288)
+  uint32_t T[10];
+  asm("v_mov_b32 %0, %10\n\t"
+      "v_add_co_u32_e32 %1, vcc, %11, %18\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %12, %19, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %13, %20, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %14, %21, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %15, %22, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %16, %23, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %17, %24, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %8, vcc, 0, %25, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %9, vcc, 0, %26, vcc"
+      : "=&v"(T[0]), "=&v"(T[1]), "=&v"(T[2]), "=&v"(T[3]), "=&v"(T[4]), "=&v"(T[5]), "=&v"(T[6]), "=&v"(T[7]),
+        "=&v"(T[8]), "=&v"(T[9])
+      : "v"(L[0]), "v"(L[1]), "v"(L[2]), "v"(L[3]), "v"(L[4]), "v"(L[5]), "v"(L[6]), "v"(L[7]),
+        "v"(H[0]), "v"(H[1]), "v"(H[2]), "v"(H[3]), "v"(H[4]), "v"(H[5]), "v"(H[6]), "v"(H[7]), "v"(0u)
+      : "vcc");
+  // P_i = 977*H_i + T_i  (< 2^42), independent
+  uint64_t P[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) P[i] = (uint64_t)H[i] * 977u + T[i];
+  // R = sum P_i 2^(32i) + (T9:T8) 2^256 : one carry chain; top = R9:R8 < 3 * 2^32
+  uint32_t R[8], R8, R9;
+  asm("v_mov_b32 %0, %10\n\t"
+      "v_add_co_u32_e32 %1, vcc, %11, %12\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %13, %14, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %15, %16, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %17, %18, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %19, %20, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %21, %22, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %23, %24, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %8, vcc, %25, %26, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %9, vcc, 0, %27, vcc"
+      : "=&v"(R[0]), "=&v"(R[1]), "=&v"(R[2]), "=&v"(R[3]), "=&v"(R[4]), "=&v"(R[5]), "=&v"(R[6]), "=&v"(R[7]),
+        "=&v"(R8), "=&v"(R9)
+      : "v"((uint32_t)P[0]),
+        "v"((uint32_t)P[1]), "v"((uint32_t)(P[0] >> 32)),
+        "v"((uint32_t)P[2]), "v"((uint32_t)(P[1] >> 32)),
+        "v"((uint32_t)P[3]), "v"((uint32_t)(P[2] >> 32)),
+        "v"((uint32_t)P[4]), "v"((uint32_t)(P[3] >> 32)),
+        "v"((uint32_t)P[5]), "v"((uint32_t)(P[4] >> 32)),
+        "v"((uint32_t)P[6]), "v"((uint32_t)(P[5] >> 32)),
+        "v"((uint32_t)P[7]), "v"((uint32_t)(P[6] >> 32)),
+        "v"(T[8]), "v"((uint32_t)(P[7] >> 32)), "v"(T[9])
+      : "vcc");
+  // second fold: top = R9:R8 (< 3 * 2^32); add top*977 at limb 0 and top*2^32 at limb 1
+  const uint64_t u = (uint64_t)R8 * 977u + (uint64_t)(R9 * 977u) * 0x100000000ull;   // < 2^44
+  const uint64_t w = (uint64_t)(uint32_t)(u >> 32) + R8;                              // limb-1 addend
+  const uint32_t w2 = (uint32_t)(w >> 32) + R9;                                       // limb-2 addend (<= 3)
+  uint32_t c;
+  asm("v_add_co_u32_e32 %0, vcc, %0, %9\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %1, %10, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %2, %11, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %4, vcc, 0, %4, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %5, vcc, 0, %5, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %7, vcc, 0, %7, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %8, vcc, 0, %12, vcc"
+      : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]), "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]), "=&v"(c)
+      : "v"((uint32_t)u), "v"((uint32_t)w), "v"(w2), "v"(0u)
+      : "vcc");
+  // c = 1 only when R wrapped past 2^256, leaving R < 2^67: add 2^256 mod p = 2^32 + 977 once
+  // more (limbs 0..3 suffice: the sum stays < 2^68).
+  const uint32_t k0 = c * 977u;
+  asm("v_add_co_u32_e32 %0, vcc, %0, %4\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %1, %5, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %3, vcc, 0, %3, vcc"
+      : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3])
+      : "v"(k0), "v"(c)
+      : "vcc");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = R[i];
+}
+
+// Production multiply/square: seeded-column schedule (fm_mul512x / fm_sqr512x).
+// Schedules: 0 = column shuffle, 1 = seeded columns folded at the end, 2 = folded as they complete.
+#ifndef KHB_MUL_IMPL
+#define KHB_MUL_IMPL 1
+#endif
+#ifndef KHB_SQR_IMPL
+#define KHB_SQR_IMPL 1
+#endif
+FM_DEV void fm_mul(Fe& r, const Fe& a, const Fe& b) {
+  uint32_t t[16];
+#if KHB_MUL_IMPL == 0
+  fm_mul512(t, a.v, b.v);
+#elif KHB_MUL_IMPL == 1
+  fm_mul512x(t, a.v, b.v);
+#else
+  fm_mul512p(t, a.v, b.v);
+#endif
+  fm_reduce(r, t);
+}
+
+FM_DEV void fm_sqr(Fe& r, const Fe& a) {
+  uint32_t t[16];
+#if KHB_SQR_IMPL == 0
+  fm_mul512(t, a.v, a.v);
+#elif KHB_SQR_IMPL == 1
+  fm_sqr512x(t, a.v);
+#else
+  fm_sqr512p(t, a.v);
+#endif
+  fm_reduce(r, t);
+}
+
+// Previous schedule (column shuffle, squaring as a general product), kept as the
+// microbenchmark / exactness baseline (tools/microbench/fmbench.hip).
+FM_DEV void fm_mul_shuffle(Fe& r, const Fe& a, const Fe& b) {
+  uint32_t t[16];
+  fm_mul512(t, a.v, b.v);
+  fm_reduce(r, t);
+}
+
+FM_DEV void fm_sqr_generic(Fe& r, const Fe& a) {
+  uint32_t t[16];
+  fm_mul512(t, a.v, a.v);
+  fm_reduce(r, t);
+}
+
+// a - b mod p for a < 2^256, b < p.
+FM_DEV void fm_sub(Fe& r, const Fe& a, const Fe& b) {
+  uint32_t d[8], m, k0, k1;
+  asm("v_sub_co_u32_e32 %0, vcc, %11, %19\n\t"
+      "s_nop 0\n\t"
+      "v_subb_co_u32_e32 %1, vcc, %12, %20, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_subb_co_u32_e32 %2, vcc, %13, %21, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_subb_co_u32_e32 %3, vcc, %14, %22, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_subb_co_u32_e32 %4, vcc, %15, %23, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_subb_co_u32_e32 %5, vcc, %16, %24, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_subb_co_u32_e32 %6, vcc, %17, %25, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_subb_co_u32_e32 %7, vcc, %18, %26, vcc\n\t"
+      // m = borrow ? 0xffffffff : 0 ; subtract (0x1000003D1 & m), i.e. add p on borrow
+      "s_nop 0\n\t"
+      "v_subb_co_u32_e32 %8, vcc, 0, %27, vcc\n\t"
+      "v_and_b32_e32 %9, 0x3d1, %8\n\t"
+      "v_and_b32_e32 %10, 1, %8\n\t"
+      "v_sub_co_u32_e32 %0, vcc, %0, %9\n\t"
+      "s_nop 0\n\t"
+      "v_subb_co_u32_e32 %1, vcc, %1, %10, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_subbrev_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_subbrev_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_subbrev_co_u32_e32 %4, vcc, 0, %4, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_subbrev_co_u32_e32 %5, vcc, 0, %5, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_subbrev_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_subbrev_co_u32_e32 %7, vcc, 0, %7, vcc"
+      : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]), "=&v"(d[6]), "=&v"(d[7]),
+        "=&v"(m), "=&v"(k0), "=&v"(k1)
+      : "v"(a.v[0]), "v"(a.v[1]), "v"(a.v[2]), "v"(a.v[3]), "v"(a.v[4]), "v"(a.v[5]), "v"(a.v[6]), "v"(a.v[7]),
+        "v"(b.v[0]), "v"(b.v[1]), "v"(b.v[2]), "v"(b.v[3]), "v"(b.v[4]), "v"(b.v[5]), "v"(b.v[6]), "v"(b.v[7]),
+        "v"(0u)
+      : "vcc");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = d[i];
+}
+
+// r = a + 0x1000003D1 (mod 2^256) with carry-out, as a chain (the "subtract p" step).
+FM_DEV uint32_t fm_add_k(uint32_t t[8], const uint32_t s[8]) {
+  uint32_t c;
+  asm("v_add_co_u32_e32 %0, vcc, 0x3d1, %9\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 1, %10, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, 0, %11, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %3, vcc, 0, %12, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %4, vcc, 0, %13, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %5, vcc, 0, %14, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %6, vcc, 0, %15, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %7, vcc, 0, %16, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %8, vcc, 0, %17, vcc"
+      : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7]),
+        "=&v"(c)
+      : "v"(s[0]), "v"(s[1]), "v"(s[2]), "v"(s[3]), "v"(s[4]), "v"(s[5]), "v"(s[6]), "v"(s[7]), "v"(0u)
+      : "vcc");
+  return c;
+}
+
+// canonical a mod p for a < 2^256
+FM_DEV void fm_canon(Fe& r, const Fe& a) {
+  uint32_t t[8];
+  const uint32_t c = fm_add_k(t, a.v);
+  const bool sel = c != 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = sel ? t[i] : a.v[i];
+}
+
+// a + b mod p, a, b < p, canonical result
+FM_DEV void fm_add(Fe& r, const Fe& a, const Fe& b) {
+  uint32_t s[8], c;
+  asm("v_add_co_u32_e32 %0, vcc, %9, %17\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %10, %18, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %11, %19, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %12, %20, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %13, %21, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %14, %22, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %15, %23, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %16, %24, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %8, vcc, 0, %25, vcc"
+      : "=&v"(s[0]), "=&v"(s[1]), "=&v"(s[2]), "=&v"(s[3]), "=&v"(s[4]), "=&v"(s[5]), "=&v"(s[6]), "=&v"(s[7]),
+        "=&v"(c)
+      : "v"(a.v[0]), "v"(a.v[1]), "v"(a.v[2]), "v"(a.v[3]), "v"(a.v[4]), "v"(a.v[5]), "v"(a.v[6]), "v"(a.v[7]),
+        "v"(b.v[0]), "v"(b.v[1]), "v"(b.v[2]), "v"(b.v[3]), "v"(b.v[4]), "v"(b.v[5]), "v"(b.v[6]), "v"(b.v[7]),
+        "v"(0u)
+      : "vcc");
+  uint32_t t[8];
+  const uint32_t ct = fm_add_k(t, s);
+  const bool sel = (c | ct) != 0;    // a+b >= p  <=>  carry out of a+b or of (a+b mod 2^256)+K
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = sel ? t[i] : s[i];
+}
+
+FM_DEV void fm_sqr_n(Fe& r, const Fe& a, int n) {
+  r = a;
+  for (int i = 0; i < n; ++i) fm_sqr(r, r);
+}
+
+// a^(p-2) (inv(0) = 0); lazy result (congruent, < 2^256).
+FM_DEV void fm_inv(Fe& r, const Fe& a) {
+  Fe x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223, t;
+  fm_sqr(x2, a);            fm_mul(x2, x2, a);
+  fm_sqr(x3, x2);           fm_mul(x3, x3, a);
+  fm_sqr_n(x6, x3, 3);      fm_mul(x6, x6, x3);
+  fm_sqr_n(x9, x6, 3);      fm_mul(x9, x9, x3);
+  fm_sqr_n(x11, x9, 2);     fm_mul(x11, x11, x2);
+  fm_sqr_n(x22, x11, 11);   fm_mul(x22, x22, x11);
+  fm_sqr_n(x44, x22, 22);   fm_mul(x44, x44, x22);
+  fm_sqr_n(x88, x44, 44);   fm_mul(x88, x88, x44);
+  fm_sqr_n(x176, x88, 88);  fm_mul(x176, x176, x88);
+  fm_sqr_n(x220, x176, 44); fm_mul(x220, x220, x44);
+  fm_sqr_n(x223, x220, 3);  fm_mul(x223, x223, x3);
+  fm_sqr_n(t, x223, 23);    fm_mul(t, t, x22);
+  fm_sqr_n(t, t, 5);        fm_mul(t, t, a);
+  fm_sqr_n(t, t, 3);        fm_mul(t, t, x2);
+  fm_sqr_n(t, t, 2);        fm_mul(r, t, a);
+}
+
+}  // namespace khb

@@ -153,10 +153,10 @@ void confirm(Shared& S, const Batch& b, std::vector<khb_cand>& cands, int thread
   if (S.n_found == (int)S.targets.size()) S.stop = true;   // "All points were found"
 }
 
-uint32_t batch_chunks(const Tables& T, const SearchConfig& cfg, size_t ntargets) {
+uint32_t batch_chunks(const Tables& T, const SearchConfig& cfg, size_t ntargets, uint32_t ctx_lanes) {
   if (cfg.chunks_per_batch) return cfg.chunks_per_batch;
   const uint64_t lanes_per_job = (T.geo.cycles + T.gpl - 1) / T.gpl;
-  const uint64_t lanes = cfg.lanes ? cfg.lanes : 256u * 8u * 64u;
+  const uint64_t lanes = ctx_lanes ? ctx_lanes : 256u * 8u * 64u;
   const uint64_t jobs = (2ull * lanes + lanes_per_job - 1) / lanes_per_job;    // ~2 work items per lane
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(jobs / std::max<size_t>(1, ntargets), 65536));
 }
@@ -173,7 +173,7 @@ void device_thread(Shared& S, khb_ctx* ctx) {
   };
   const Tables& T = S.T;
   const uint32_t cycles = (uint32_t)T.geo.cycles;
-  const uint32_t want = batch_chunks(T, S.cfg, S.targets.size());
+  const uint32_t want = batch_chunks(T, S.cfg, S.targets.size(), khb_lanes(ctx));
   const int threads = S.cfg.check_threads > 0 ? S.cfg.check_threads
                                                : (int)std::max(2u, std::min(16u, std::thread::hardware_concurrency()));
   std::vector<khb_cand> cbuf(1u << 20);

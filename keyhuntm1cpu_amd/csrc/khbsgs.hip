@@ -19,6 +19,7 @@
 #include <new>
 #include "../../include/khbsgs.h"
 #include "device/fe.hpp"
+#include "device/fe_asm.hpp"
 #include "device/bloom_probe.hpp"
 
 using namespace khb;
@@ -29,6 +30,15 @@ struct AffPt {
   Fe x, y;
 };
 
+#ifndef KHB_PROBE_MODE
+#define KHB_PROBE_MODE 0          // 0 = product; 1..3 = perf experiments (tools/perf_variants.py)
+#endif
+#ifndef KHB_PROBE_BITS
+#define KHB_PROBE_BITS 1          // bloom bits per round trip in a width-1 drain (2 and 4 measured slower)
+#endif
+#ifndef KHB_WAVES_PER_SIMD
+#define KHB_WAVES_PER_SIMD 4      // occupancy target of k_giant_scan (launch bounds); w4 measured best
+#endif
 constexpr uint32_t kBlock = 256;
 constexpr uint32_t kHalf = KHB_GROUP / 2;            // 512
 constexpr uint32_t kCandCap = 1u << 20;
@@ -54,80 +64,244 @@ __device__ __forceinline__ void emit_cand(const ScanArgs& A, uint32_t job, uint3
   if (k < A.cand_cap) A.cand[k] = khb_cand{job, a};
 }
 
+// ---- level-1 probe with a per-wave survivor queue ---------------------------------------------
+// Every x pays the first XXH64 and one bloom bit.  The ~50 % whose first bit is set are pushed to
+// a per-wave LDS queue (x, a, job, giant-step index); whenever 64 are queued the whole wave
+// finishes 64 of them together (second XXH64 + remaining bits, bloom_rest).  Without the queue a
+// wave would run the second hash and the dependent bit loads whenever ANY of its lanes survived,
+// i.e. for every x, with one memory round trip per bit per probe site.
+#ifndef KHB_DRAIN_WIDTH
+#define KHB_DRAIN_WIDTH 1         // queued entries finished per lane per drain (1 or 2; 2 measured no faster)
+#endif
+constexpr uint32_t kDrainAt = 64 * KHB_DRAIN_WIDTH;   // drain threshold (entries)
+constexpr uint32_t kQCap = kDrainAt + 64;           // entries per wave: < kDrainAt resident + <= 64 pushed
+constexpr uint32_t kQWords = 12;           // x[8], a lo, a hi, job, step index (SoA in LDS)
+constexpr uint32_t kWavesPerBlock = kBlock / 64;
+
+// The count lives in LDS, not in a register: lanes of a wave may diverge (the ragged last lane of
+// a job, the tail of the item loop), and a register copy would go stale in the inactive lanes.
+struct ProbeQueue {
+  uint32_t* q;            // this wave's LDS region: kQWords arrays of kQCap words
+  volatile uint32_t* n;   // this wave's queued-entry count (LDS)
+};
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// Read queued entry k (x, a, job, step).
+__device__ __forceinline__ void q_read(const ProbeQueue& Q, uint32_t k, Fe& x, uint64_t& a, uint32_t& job,
+                                       uint32_t& step) {
+#pragma unroll
+  for (int d = 0; d < 8; ++d) x.v[d] = Q.q[d * kQCap + k];
+  a = (uint64_t)Q.q[8 * kQCap + k] | ((uint64_t)Q.q[9 * kQCap + k] << 32);
+  job = Q.q[10 * kQCap + k];
+  step = Q.q[11 * kQCap + k];
+}
+
+// Finish up to min(n, KHB_DRAIN_WIDTH x active lanes) queued entries (the newest ones), while
+// n >= threshold.  With width 2 every lane carries two entries through one interleaved bit loop.
+__device__ __forceinline__ void q_drain(const ScanArgs& A, ProbeQueue& Q, uint32_t threshold) {
+  for (;;) {
+    const uint32_t n = *Q.n;
+    if (n < threshold || n == 0) break;
+    const uint64_t em = __ballot(1);
+    const uint32_t na = (uint32_t)__popcll(em);
+    const uint32_t take = min(n, KHB_DRAIN_WIDTH * na);
+    const uint32_t r = lane_rank(em);
+    *Q.n = n - take;
+    asm volatile("" ::: "memory");
+#if KHB_DRAIN_WIDTH == 1
+    if (r < take) {
+      Fe x;
+      uint64_t a;
+      uint32_t job, step;
+      q_read(Q, n - take + r, x, a, job, step);
+      uint64_t w[4];
+      x_words(w, x);
+      if (bloom_rest_r<KHB_PROBE_BITS>(sub_bloom(A.bloom, A.geom, x), A.geom, w, a)) emit_cand(A, job, step);
+    }
+#else
+    if (r < take) {
+      const uint32_t k1 = n - take + r, k2 = k1 + na;
+      bool ok1 = true, ok2 = r + na < take;
+      Fe x1, x2;
+      uint64_t a1, a2;
+      uint32_t job1, step1, job2, step2;
+      q_read(Q, k1, x1, a1, job1, step1);
+      q_read(Q, ok2 ? k2 : k1, x2, a2, job2, step2);
+      uint64_t w1[4], w2[4];
+      x_words(w1, x1);
+      x_words(w2, x2);
+      bloom_rest_pair(A.geom, sub_bloom(A.bloom, A.geom, x1), w1, a1, ok1, sub_bloom(A.bloom, A.geom, x2), w2, a2,
+                      ok2);
+      if (ok1) emit_cand(A, job1, step1);
+      if (ok2) emit_cand(A, job2, step2);
+    }
+#endif
+    asm volatile("" ::: "memory");
+  }
+}
+
+// Queue x if its first bloom bit (hash a) is set.
+__device__ __forceinline__ void q_push(ProbeQueue& Q, bool hit, const Fe& x, uint64_t a, uint32_t job,
+                                       uint32_t step) {
+  const uint64_t m = __ballot(hit);
+  const uint32_t n = *Q.n;
+  if (hit) {
+    const uint32_t k = n + lane_rank(m);
+#pragma unroll
+    for (int d = 0; d < 8; ++d) Q.q[d * kQCap + k] = x.v[d];
+    Q.q[8 * kQCap + k] = (uint32_t)a;
+    Q.q[9 * kQCap + k] = (uint32_t)(a >> 32);
+    Q.q[10 * kQCap + k] = job;
+    Q.q[11 * kQCap + k] = step;
+  }
+  asm volatile("" ::: "memory");
+  *Q.n = n + (uint32_t)__popcll(m);
+}
+
+__device__ __forceinline__ bool first_bit(const ScanArgs& A, const Fe& x, uint64_t& a) {
+  uint64_t w[4];
+  x_words(w, x);
+  a = xxh64_32(w, KHB_BLOOM_SEED);
+  return test_bit(sub_bloom(A.bloom, A.geom, x), mod_bits(a, A.geom));
+}
+
 template <bool DUMP>
-__device__ __forceinline__ void probe(const ScanArgs& A, const Fe& x, uint32_t job, uint32_t j, uint32_t t) {
+__device__ __forceinline__ void probe(const ScanArgs& A, ProbeQueue& Q, const Fe& x, uint32_t job, uint32_t j,
+                                      uint32_t t) {
   if (DUMP) {
     uint8_t* o = A.xdump + ((uint64_t)(j - A.group_begin) * KHB_GROUP + t) * 32;
     fe_to_be(o, x);
   } else {
-    if (bloom_probe_x(A.bloom, A.geom, x)) emit_cand(A, job, j * KHB_GROUP + t);
+#if KHB_PROBE_MODE == 0
+    uint64_t a;
+    const bool hit = first_bit(A, x, a);
+    q_push(Q, hit, x, a, job, j * KHB_GROUP + t);
+    q_drain(A, Q, kDrainAt);
+#elif KHB_PROBE_MODE == 1      // perf experiment: first hash only, no bloom access
+    uint64_t w[4];
+    x_words(w, x);
+    if (xxh64_32(w, KHB_BLOOM_SEED) == 0x0123456789abcdefull) emit_cand(A, job, j * KHB_GROUP + t);
+#elif KHB_PROBE_MODE == 2      // perf experiment: first hash + first bit only
+    uint64_t w[4];
+    x_words(w, x);
+    const uint64_t a = xxh64_32(w, KHB_BLOOM_SEED);
+    const uint8_t* bf = sub_bloom(A.bloom, A.geom, x);
+    const uint64_t pos = mod_bits(a, A.geom);
+    if ((bf[pos >> 3] >> (pos & 7)) & 1u & (a == 0x0123456789abcdefull)) emit_cand(A, job, j * KHB_GROUP + t);
+#else                          // perf experiment: no probe at all
+    if (x.v[0] == 0x01234567u && x.v[1] == 0x89abcdefu) emit_cand(A, job, j * KHB_GROUP + t);
+#endif
   }
 }
 
-// One reference group (keyhunt.cpp:3873-3999) centred on C; advances C to the next centre.
+// The two points of one backward step (C - GSn[i], C + GSn[i]): both first hashes are computed
+// before either bloom bit is awaited, so the two loads share one memory round trip.
 template <bool DUMP>
-__device__ __forceinline__ void scan_group(const ScanArgs& A, AffPt& C, uint32_t job, uint32_t j, Fe* scr) {
+__device__ __forceinline__ void probe_pair(const ScanArgs& A, ProbeQueue& Q, const Fe& x1, const Fe& x2,
+                                           uint32_t job, uint32_t j, uint32_t t1, uint32_t t2) {
+#if KHB_PROBE_MODE == 0
+  if (!DUMP) {
+    uint64_t a1, a2;
+    const bool h1 = first_bit(A, x1, a1);
+    const bool h2 = first_bit(A, x2, a2);
+    q_push(Q, h1, x1, a1, job, j * KHB_GROUP + t1);
+    q_drain(A, Q, kDrainAt);
+    q_push(Q, h2, x2, a2, job, j * KHB_GROUP + t2);
+    q_drain(A, Q, kDrainAt);
+    return;
+  }
+#endif
+  probe<DUMP>(A, Q, x1, job, j, t1);
+  probe<DUMP>(A, Q, x2, job, j, t2);
+}
+
+// One reference group (keyhunt.cpp:3873-3999) centred on C; advances C to the next centre.
+// C is canonical on entry and exit; products are lazy (< 2^256) and every x is canonicalised
+// before it is hashed or dumped (fe_asm.hpp value contract).
+template <bool DUMP>
+__device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, AffPt& C, uint32_t job, uint32_t j,
+                                           Fe* scr) {
   const uint32_t S = A.stride;
   const AffPt* __restrict__ gsn = A.gsn;
   Fe acc, dx;
   // forward pass: prefix products of dx[i] = GSn[i].x - C.x (i < 512) and _2GSn.x - C.x
-  fe_sub(acc, gsn[0].x, C.x);
+  fm_sub(acc, gsn[0].x, C.x);
   scr[0] = acc;
   for (uint32_t i = 1; i < kHalf; ++i) {
-    fe_sub(dx, gsn[i].x, C.x);
-    fe_mul(acc, acc, dx);
+    fm_sub(dx, gsn[i].x, C.x);
+    fm_mul(acc, acc, dx);
     scr[(size_t)i * S] = acc;
   }
-  fe_sub(dx, gsn[kHalf].x, C.x);
-  fe_mul(acc, acc, dx);
-  const bool degenerate = fe_is_zero(acc);
+  fm_sub(dx, gsn[kHalf].x, C.x);
+  fm_mul(acc, acc, dx);
+  Fe accc;
+  fm_canon(accc, acc);
+  const bool degenerate = fe_is_zero(accc);
   Fe inv;
-  fe_inv(inv, acc);                       // 0 when degenerate -> every inverse 0, as the reference
+  fm_inv(inv, acc);                       // == 0 (mod p) when degenerate -> every inverse 0, as the reference
   // i = 512: inverse of _2GSn.x - C.x, kept for the next centre
-  Fe inv2, pre;
-  pre = scr[(size_t)(kHalf - 1) * S];
-  fe_mul(inv2, inv, pre);
-  fe_mul(inv, inv, dx);
+  Fe pre;
+  {
+    // i = 512's inverse is only needed for the next centre: park it in prefix slot 511, which
+    // is read exactly once (here), instead of holding 8 VGPRs through the backward loop.
+    Fe inv2;
+    pre = scr[(size_t)(kHalf - 1) * S];
+    fm_mul(inv2, inv, pre);
+    scr[(size_t)(kHalf - 1) * S] = inv2;
+    asm volatile("" ::: "memory");
+  }
+  fm_mul(inv, inv, dx);
   for (int i = (int)kHalf - 1; i >= 0; --i) {
     Fe idx;
     if (i > 0) {
       pre = scr[(size_t)(i - 1) * S];
-      fe_mul(idx, inv, pre);
-      fe_sub(dx, gsn[i].x, C.x);
-      fe_mul(inv, inv, dx);
+      fm_mul(idx, inv, pre);
+      fm_sub(dx, gsn[i].x, C.x);
+      fm_mul(inv, inv, dx);
     } else {
       idx = inv;
     }
-    Fe u, s, x;
-    fe_add(u, C.x, gsn[i].x);             // x = s^2 - C.x - GSn.x
+    Fe u, s, x1;
+    fm_add(u, C.x, gsn[i].x);             // x = s^2 - (C.x + GSn.x)
     // C - GSn[i]: s = (-GSn.y - C.y)/dx; only s^2 is needed
-    fe_add(s, gsn[i].y, C.y);
-    fe_mul(s, s, idx);
-    fe_sqr(x, s);
-    fe_sub(x, x, u);
-    probe<DUMP>(A, x, job, j, kHalf - 1 - (uint32_t)i);
+    fm_add(s, gsn[i].y, C.y);
+    fm_mul(s, s, idx);
+    fm_sqr(x1, s);
+    fm_sub(x1, x1, u);
+    fm_canon(x1, x1);
     if (i < (int)kHalf - 1) {
       // C + GSn[i]: s = (GSn.y - C.y)/dx
-      fe_sub(s, gsn[i].y, C.y);
-      fe_mul(s, s, idx);
-      fe_sqr(x, s);
-      fe_sub(x, x, u);
-      probe<DUMP>(A, x, job, j, kHalf + 1 + (uint32_t)i);
+      Fe x2;
+      fm_sub(s, gsn[i].y, C.y);
+      fm_mul(s, s, idx);
+      fm_sqr(x2, s);
+      fm_sub(x2, x2, u);
+      fm_canon(x2, x2);
+      probe_pair<DUMP>(A, Q, x1, x2, job, j, kHalf - 1 - (uint32_t)i, kHalf + 1 + (uint32_t)i);
+    } else {
+      probe<DUMP>(A, Q, x1, job, j, kHalf - 1 - (uint32_t)i);
     }
   }
-  probe<DUMP>(A, C.x, job, j, kHalf);
+  probe<DUMP>(A, Q, C.x, job, j, kHalf);
   // next centre: C + _2GSn with y (keyhunt.cpp:3986-3999)
   {
+    asm volatile("" ::: "memory");
+    const Fe inv2 = scr[(size_t)(kHalf - 1) * S];
     const AffPt& g2 = gsn[kHalf];
     Fe s, nx, ny;
-    fe_sub(s, g2.y, C.y);
-    fe_mul(s, s, inv2);
-    fe_sqr(nx, s);
-    fe_sub(nx, nx, C.x);
-    fe_sub(nx, nx, g2.x);
-    fe_sub(ny, g2.x, nx);
-    fe_mul(ny, ny, s);
-    fe_sub(ny, ny, g2.y);
+    fm_sub(s, g2.y, C.y);
+    fm_mul(s, s, inv2);
+    fm_sqr(nx, s);
+    fm_sub(nx, nx, C.x);
+    fm_sub(nx, nx, g2.x);
+    fm_canon(nx, nx);
+    fm_sub(ny, g2.x, nx);
+    fm_mul(ny, ny, s);
+    fm_sub(ny, ny, g2.y);
+    fm_canon(ny, ny);
     C.x = nx;
     C.y = ny;
   }
@@ -140,26 +314,33 @@ __device__ __forceinline__ void scan_group(const ScanArgs& A, AffPt& C, uint32_t
 // AddDirect (SECP256K1.cpp:242-265) with its own inversion; used once per lane.
 __device__ __forceinline__ bool add_direct(AffPt& r, const AffPt& p1, const AffPt& p2) {
   Fe dy, dx, s, x, y;
-  fe_sub(dy, p2.y, p1.y);
-  fe_sub(dx, p2.x, p1.x);
+  fm_sub(dy, p2.y, p1.y);
+  fm_sub(dx, p2.x, p1.x);
   const bool degenerate = fe_is_zero(dx);
-  fe_inv(dx, dx);
-  fe_mul(s, dy, dx);
-  fe_sqr(x, s);
-  fe_sub(x, x, p1.x);
-  fe_sub(x, x, p2.x);
-  fe_sub(y, p2.x, x);
-  fe_mul(y, y, s);
-  fe_sub(y, y, p2.y);
+  fm_inv(dx, dx);
+  fm_mul(s, dy, dx);
+  fm_sqr(x, s);
+  fm_sub(x, x, p1.x);
+  fm_sub(x, x, p2.x);
+  fm_canon(x, x);
+  fm_sub(y, p2.x, x);
+  fm_mul(y, y, s);
+  fm_sub(y, y, p2.y);
+  fm_canon(y, y);
   r.x = x;
   r.y = y;
   return degenerate;
 }
 
 template <bool DUMP>
-__global__ __launch_bounds__(kBlock, 2) void k_giant_scan(ScanArgs A) {
+__global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanArgs A) {
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   Fe* scr = A.scratch + lane;
+  __shared__ uint32_t s_queue[DUMP ? 1 : kWavesPerBlock][DUMP ? 1 : kQWords * kQCap];
+  __shared__ uint32_t s_count[kWavesPerBlock];
+  const uint32_t wave = DUMP ? 0 : threadIdx.x >> 6;
+  ProbeQueue Q{s_queue[wave], &s_count[wave]};
+  if (!DUMP) *Q.n = 0;
   for (uint64_t item = lane; item < A.n_items; item += A.stride) {
     const uint32_t job = (uint32_t)(item / A.lanes_per_job);
     const uint32_t m = (uint32_t)(item % A.lanes_per_job);
@@ -173,21 +354,24 @@ __global__ __launch_bounds__(kBlock, 2) void k_giant_scan(ScanArgs A) {
         if (k < A.degen_cap) A.degen[k] = khb_degenerate{job, g0 | 0x80000000u};
       }
     }
-    for (uint32_t j = g0; j < g1; ++j) scan_group<DUMP>(A, C, job, j, scr);
+    for (uint32_t j = g0; j < g1; ++j) scan_group<DUMP>(A, Q, C, job, j, scr);
   }
+  if (!DUMP) q_drain(A, Q, 1);   // the wave has reconverged: finish what is still queued
 }
 
+// Field self-test: the fast (fe_asm.hpp) operations, results canonicalised.
 __global__ void k_field_op(int op, const Fe* __restrict__ a, const Fe* __restrict__ b, Fe* __restrict__ r, uint32_t n) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Fe x = a[i], y = b[i], z;
   switch (op) {
-    case 0: fe_mul(z, x, y); break;
-    case 1: fe_sqr(z, x); break;
-    case 2: fe_add(z, x, y); break;
-    case 3: fe_sub(z, x, y); break;
-    default: fe_inv(z, x); break;
+    case 0: fm_mul(z, x, y); break;
+    case 1: fm_sqr(z, x); break;
+    case 2: fm_add(z, x, y); break;
+    case 3: fm_sub(z, x, y); break;
+    default: fm_inv(z, x); break;
   }
+  fm_canon(z, z);
   r[i] = z;
 }
 
@@ -303,6 +487,7 @@ const char* khb_strerror(int code) {
 
 int khb_last_hip_error(const khb_ctx* c) { return c ? c->last_hip : 0; }
 void* khb_stream(khb_ctx* c) { return c ? (void*)c->stream : nullptr; }
+uint32_t khb_lanes(const khb_ctx* c) { return c ? c->lanes : 0; }
 
 int khb_device_count(int* n) {
   if (!n) return KHB_EINVAL;
@@ -323,7 +508,7 @@ int khb_open(int device, uint32_t lanes, khb_ctx** out) {
   khb_ctx* c = new (std::nothrow) khb_ctx();
   if (!c) return KHB_ENOMEM;
   c->device = device;
-  if (lanes == 0) lanes = (uint32_t)prop.multiProcessorCount * 8u * 64u;
+  if (lanes == 0) lanes = (uint32_t)prop.multiProcessorCount * 4u * KHB_WAVES_PER_SIMD * 64u;   // one full residency
   lanes = (lanes + kBlock - 1) / kBlock * kBlock;
   c->lanes = lanes;
   int rc = KHB_OK;

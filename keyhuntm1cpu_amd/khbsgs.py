@@ -32,15 +32,16 @@ class Stats(C.Structure):
                 ("kernel_ms", C.c_float)]
 
 
-_lib = None
+_libs: dict[str, C.CDLL] = {}
 
 
-def lib() -> C.CDLL:
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise KhbError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build())")
-        L = C.CDLL(LIB_PATH)
+def lib(path: str | None = None) -> C.CDLL:
+    """The bound library; `path` selects an alternative build (kernel variants in tools/)."""
+    path = path or LIB_PATH
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise KhbError(f"{path} not built: run `make` (or __graft_entry__.build())")
+        L = C.CDLL(path)
         P = C.POINTER
         L.khb_device_count.argtypes = [P(C.c_int)]
         L.khb_open.argtypes = [C.c_int, C.c_uint32, P(C.c_void_p)]
@@ -50,6 +51,8 @@ def lib() -> C.CDLL:
         L.khb_last_hip_error.argtypes = [C.c_void_p]
         L.khb_stream.restype = C.c_void_p
         L.khb_stream.argtypes = [C.c_void_p]
+        L.khb_lanes.restype = C.c_uint32
+        L.khb_lanes.argtypes = [C.c_void_p]
         L.khb_load_bloom.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, C.c_uint64, C.c_uint32]
         L.khb_load_giant_table.argtypes = [C.c_void_p, C.c_char_p]
         L.khb_load_lane_offsets.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32]
@@ -60,15 +63,16 @@ def lib() -> C.CDLL:
         L.khb_dump_x.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_char_p]
         L.khb_field_op.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint32]
         L.khb_probe.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_uint32]
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
-def _check(rc: int, ctx=None) -> None:
+def _check(rc: int, ctx=None, L: C.CDLL | None = None) -> None:
     if rc != 0:
-        msg = lib().khb_strerror(rc).decode()
+        L = L or lib()
+        msg = L.khb_strerror(rc).decode()
         if ctx:
-            msg += f" (hipError {lib().khb_last_hip_error(ctx)})"
+            msg += f" (hipError {L.khb_last_hip_error(ctx)})"
         raise KhbError(f"khbsgs: {msg} [{rc}]")
 
 
@@ -81,14 +85,15 @@ def device_count() -> int:
 class Engine:
     """One libkhbsgs context (one device)."""
 
-    def __init__(self, device: int = 0, lanes: int = 0):
+    def __init__(self, device: int = 0, lanes: int = 0, lib_path: str | None = None):
+        self.L = lib(lib_path)
         self.h = C.c_void_p()
-        _check(lib().khb_open(device, lanes, C.byref(self.h)))
+        _check(self.L.khb_open(device, lanes, C.byref(self.h)), None, self.L)
         self.gpl = 0
 
     def close(self) -> None:
         if self.h:
-            lib().khb_close(self.h)
+            self.L.khb_close(self.h)
             self.h = C.c_void_p()
 
     def __enter__(self):
@@ -97,30 +102,33 @@ class Engine:
     def __exit__(self, *a):
         self.close()
 
+    def lanes(self) -> int:
+        return int(self.L.khb_lanes(self.h))
+
     def stream(self) -> int:
-        return int(lib().khb_stream(self.h) or 0)
+        return int(self.L.khb_stream(self.h) or 0)
 
     def load_bloom(self, bf: bytes, bytes_per_sub: int, bits: int, hashes: int) -> None:
         assert len(bf) == 256 * bytes_per_sub
-        _check(lib().khb_load_bloom(self.h, bf, bytes_per_sub, bits, hashes), self.h)
+        _check(self.L.khb_load_bloom(self.h, bf, bytes_per_sub, bits, hashes), self.h, self.L)
 
     def load_giant_table(self, gsn: bytes) -> None:
         assert len(gsn) == 513 * 64
-        _check(lib().khb_load_giant_table(self.h, gsn), self.h)
+        _check(self.L.khb_load_giant_table(self.h, gsn), self.h, self.L)
 
     def load_lane_offsets(self, offs: bytes, gpl: int) -> None:
         assert len(offs) % 64 == 0
-        _check(lib().khb_load_lane_offsets(self.h, offs, len(offs) // 64, gpl), self.h)
+        _check(self.L.khb_load_lane_offsets(self.h, offs, len(offs) // 64, gpl), self.h, self.L)
         self.gpl = gpl
 
     def submit(self, centres: bytes, group_begin: int, group_count: int) -> None:
-        _check(lib().khb_submit(self.h, centres, len(centres) // 64, group_begin, group_count), self.h)
+        _check(self.L.khb_submit(self.h, centres, len(centres) // 64, group_begin, group_count), self.h, self.L)
 
     def collect(self, cap: int = 1 << 20):
         cand = (Cand * cap)()
         deg = (Degenerate * 4096)()
         st = Stats()
-        _check(lib().khb_collect(self.h, cand, cap, deg, 4096, C.byref(st)), self.h)
+        _check(self.L.khb_collect(self.h, cand, cap, deg, 4096, C.byref(st)), self.h, self.L)
         n = min(st.n_cand, cap)
         return ([(int(cand[i].job), int(cand[i].a)) for i in range(n)],
                 [(int(deg[i].job), int(deg[i].group)) for i in range(min(st.n_degenerate, 4096))], st)
@@ -131,17 +139,17 @@ class Engine:
 
     def dump_x(self, centre: bytes, group_begin: int, group_count: int) -> bytes:
         out = C.create_string_buffer(group_count * KHB_GROUP * 32)
-        _check(lib().khb_dump_x(self.h, centre, group_begin, group_count, out), self.h)
+        _check(self.L.khb_dump_x(self.h, centre, group_begin, group_count, out), self.h, self.L)
         return out.raw
 
     def field_op(self, op: int, a: bytes, b: bytes | None) -> bytes:
         n = len(a) // 32
         out = C.create_string_buffer(n * 32)
-        _check(lib().khb_field_op(self.h, op, a, b, out, n), self.h)
+        _check(self.L.khb_field_op(self.h, op, a, b, out, n), self.h, self.L)
         return out.raw
 
     def probe(self, xs: bytes) -> bytes:
         n = len(xs) // 32
         out = C.create_string_buffer(n)
-        _check(lib().khb_probe(self.h, xs, out, n), self.h)
+        _check(self.L.khb_probe(self.h, xs, out, n), self.h, self.L)
         return out.raw

@@ -44,6 +44,9 @@ def test_field_ops(eng):
     b = [rand_fe(rng) for _ in range(n)]
     a[0] = 0
     b[1] = 0
+    edges = [0, 1, 2, P - 1, P - 2, P - 977, 2**255, 2**256 - 2**32 - 978, 2**224 - 1, 2**32 - 1, 2**64 - 1]
+    for k, (x, y) in enumerate((x, y) for x in edges for y in edges):
+        a[2 + k], b[2 + k] = x, y
     ab = b"".join(x.to_bytes(32, "big") for x in a)
     bb = b"".join(x.to_bytes(32, "big") for x in b)
     ops = {0: lambda x, y: x * y % P, 1: lambda x, y: x * x % P, 2: lambda x, y: (x + y) % P,
@@ -125,3 +128,31 @@ def test_degenerate_group_matches_reference(eng, bs32, ora):
     assert xs == xs_ref
     _, degen, _ = eng.scan(st.be64(), 0, bs32.cycles)
     assert (0, j) in degen
+
+
+def test_candidates_ragged_lanes_match_oracle(eng, bs32, ora):
+    """Diverged waves: 62 groups per job with 4 groups per lane leaves every job's last lane two
+    groups short, and 35 jobs x 16 lanes = 560 items ends mid-wave.  The survivor queue must stay
+    consistent while only part of a wave is active."""
+    gpl = 4
+    load_tables(eng, bs32, gpl)
+    rng = random.Random(5)
+    base0 = 0x2100000000000000
+    two_n = 2 * (1 << 32)
+    keys = [base0 + rng.randrange(7 * two_n) for _ in range(5)]
+    targets = [ora.pubkey(k) for k in keys]
+    centres, ref = [], []
+    for c in range(7):
+        for t in targets:
+            st = bs32.chunk_start(base0 + c * two_n, t)
+            centres.append(st.be64())
+            cands, _, _ = bs32.scan(st, 0, 62)
+            ref.append(sorted(cands))
+    got, degen, stats = eng.scan(b"".join(centres), 0, 62)
+    assert not degen
+    assert stats.giant_steps == 35 * 62 * 1024
+    per_job = [[] for _ in centres]
+    for job, a in got:
+        per_job[job].append(a)
+    assert [sorted(x) for x in per_job] == ref
+    assert sum(len(r) for r in ref) > 0
