@@ -45,7 +45,7 @@ clean:
 .PHONY: all oracle clean
 
 # Kernel variants for A/B timing (tools/perf_variants.py); not used by the product.
-VARIANTS := w2 w4
+VARIANTS := w2 g0
 variants: $(patsubst %,$(LIBDIR)/variants/libkhbsgs_%.so,$(VARIANTS))
 $(LIBDIR)/variants/libkhbsgs_w%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
@@ -53,6 +53,9 @@ $(LIBDIR)/variants/libkhbsgs_w%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 $(LIBDIR)/variants/libkhbsgs_r%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) -DKHB_PROBE_BITS=$* -shared -o $@ $(CSRC)/khbsgs.hip
+$(LIBDIR)/variants/libkhbsgs_g%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_GSN_SCALAR=$* -shared -o $@ $(CSRC)/khbsgs.hip
 $(LIBDIR)/variants/libkhbsgs_m0s%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) -DKHB_MUL_IMPL=0 -DKHB_SQR_IMPL=$* -shared -o $@ $(CSRC)/khbsgs.hip

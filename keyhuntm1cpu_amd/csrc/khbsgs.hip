@@ -36,6 +36,9 @@ struct AffPt {
 #ifndef KHB_PROBE_BITS
 #define KHB_PROBE_BITS 1          // bloom bits per round trip in a width-1 drain (2 and 4 measured slower)
 #endif
+#ifndef KHB_GSN_SCALAR
+#define KHB_GSN_SCALAR 1          // GSn table through scalar loads
+#endif
 #ifndef KHB_WAVES_PER_SIMD
 #define KHB_WAVES_PER_SIMD 4      // occupancy target of k_giant_scan (launch bounds); w4 measured best
 #endif
@@ -218,6 +221,28 @@ __device__ __forceinline__ void probe_pair(const ScanArgs& A, ProbeQueue& Q, con
   probe<DUMP>(A, Q, x2, job, j, t2);
 }
 
+// GSn / _2GSn rows (wave-uniform index).  With KHB_GSN_SCALAR the table is read through the
+// constant address space, so rows arrive by scalar loads into SGPRs (lgkmcnt) instead of taking
+// 16 VGPRs and four vector-memory slots per backward step.
+struct GsnTable {
+  const AffPt* p;
+#if KHB_GSN_SCALAR
+  typedef const __attribute__((address_space(4))) uint32_t* CW;
+  __device__ __forceinline__ Fe ld(uint32_t word) const {
+    CW w = (CW)p + word;
+    Fe r;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r.v[k] = w[k];
+    return r;
+  }
+  __device__ __forceinline__ Fe x(uint32_t i) const { return ld(16 * i); }
+  __device__ __forceinline__ AffPt pt(uint32_t i) const { return AffPt{ld(16 * i), ld(16 * i + 8)}; }
+#else
+  __device__ __forceinline__ Fe x(uint32_t i) const { return p[i].x; }
+  __device__ __forceinline__ AffPt pt(uint32_t i) const { return p[i]; }
+#endif
+};
+
 // One reference group (keyhunt.cpp:3873-3999) centred on C; advances C to the next centre.
 // C is canonical on entry and exit; products are lazy (< 2^256) and every x is canonicalised
 // before it is hashed or dumped (fe_asm.hpp value contract).
@@ -225,17 +250,26 @@ template <bool DUMP>
 __device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, AffPt& C, uint32_t job, uint32_t j,
                                            Fe* scr) {
   const uint32_t S = A.stride;
-  const AffPt* __restrict__ gsn = A.gsn;
+  // GSn rows are wave-uniform: read them through the constant address space so they arrive by
+  // scalar loads (SGPRs, lgkmcnt) instead of occupying 16 VGPRs and the vector-memory queue.
+  const GsnTable gsn{A.gsn};
   Fe acc, dx;
   // forward pass: prefix products of dx[i] = GSn[i].x - C.x (i < 512) and _2GSn.x - C.x
-  fm_sub(acc, gsn[0].x, C.x);
+  {
+    const Fe gx = gsn.x(0);
+    fm_sub(acc, gx, C.x);
+  }
   scr[0] = acc;
   for (uint32_t i = 1; i < kHalf; ++i) {
-    fm_sub(dx, gsn[i].x, C.x);
+    const Fe gx = gsn.x(i);
+    fm_sub(dx, gx, C.x);
     fm_mul(acc, acc, dx);
     scr[(size_t)i * S] = acc;
   }
-  fm_sub(dx, gsn[kHalf].x, C.x);
+  {
+    const Fe gx = gsn.x(kHalf);
+    fm_sub(dx, gx, C.x);
+  }
   fm_mul(acc, acc, dx);
   Fe accc;
   fm_canon(accc, acc);
@@ -259,15 +293,17 @@ __device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, Aff
     if (i > 0) {
       pre = scr[(size_t)(i - 1) * S];
       fm_mul(idx, inv, pre);
-      fm_sub(dx, gsn[i].x, C.x);
+      const Fe gx = gsn.x(i);
+      fm_sub(dx, gx, C.x);
       fm_mul(inv, inv, dx);
     } else {
       idx = inv;
     }
     Fe u, s, x1;
-    fm_add(u, C.x, gsn[i].x);             // x = s^2 - (C.x + GSn.x)
+    const AffPt g = gsn.pt(i);
+    fm_add(u, C.x, g.x);                  // x = s^2 - (C.x + GSn.x)
     // C - GSn[i]: s = (-GSn.y - C.y)/dx; only s^2 is needed
-    fm_add(s, gsn[i].y, C.y);
+    fm_add(s, g.y, C.y);
     fm_mul(s, s, idx);
     fm_sqr(x1, s);
     fm_sub(x1, x1, u);
@@ -275,7 +311,7 @@ __device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, Aff
     if (i < (int)kHalf - 1) {
       // C + GSn[i]: s = (GSn.y - C.y)/dx
       Fe x2;
-      fm_sub(s, gsn[i].y, C.y);
+      fm_sub(s, g.y, C.y);
       fm_mul(s, s, idx);
       fm_sqr(x2, s);
       fm_sub(x2, x2, u);
@@ -290,7 +326,7 @@ __device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, Aff
   {
     asm volatile("" ::: "memory");
     const Fe inv2 = scr[(size_t)(kHalf - 1) * S];
-    const AffPt& g2 = gsn[kHalf];
+    const AffPt g2 = gsn.pt(kHalf);
     Fe s, nx, ny;
     fm_sub(s, g2.y, C.y);
     fm_mul(s, s, inv2);
