@@ -58,8 +58,9 @@ def cpu_baseline(seconds: float, threads: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    # default: >= 30 s of steady state — 700 steps x 2^30 giant steps at ~44 ms
+    ap.add_argument("--steps", type=int, default=700)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--chunks", type=int, default=256, help="chunks (2N keys each) per step")
     ap.add_argument("--k", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -158,7 +159,8 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "real puzzle #66 pubkey (solved key, hash160 == tests/66.rmd), -b 66 range, sequential chunks",
-        "config": {"workload": "puzzle66 -m bsgs -b 66 -k %d (BASELINE configs[1])" % args.k,
+        "config": {"workload": "puzzle66 -m bsgs -b 66 -k %d (BASELINE configs[%s])"
+                               % (args.k, {1: "1", 4: "2"}.get(args.k, "1, k varied")),
                    "n": hex(tables.n_low), "bsgs_m": tables.m, "groups_per_chunk": tables.cycles,
                    "chunks_per_step": args.chunks, "giant_steps_per_step": per_launch_steps,
                    "parallelism": "range-partition x%d" % world, "table_build_s": round(t_build, 2),

@@ -117,3 +117,57 @@ def test_cli_rejects_bad_geometry(tmp_path):
     (tmp_path / "66.txt").write_text("13zb1hQbWVsc2S7ZTZnP2G4undNNpdh5so\n")
     r = _cli(["-m", "bsgs", "-f", "66.txt", "-b", "66"], tmp_path)
     assert r.returncode == 1 and "There is no valid data in the file" in r.stderr
+
+
+def _splitmix64(seed):
+    s = seed
+    while True:
+        s = (s + 0x9E3779B97F4A7C15) & (2**64 - 1)
+        z = s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & (2**64 - 1)
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & (2**64 - 1)
+        yield z ^ (z >> 31)
+
+
+@pytest.fixture(scope="module")
+def tables_k4():
+    t = khhost.Tables(None, 4, threads=16)
+    yield t
+    t.close()
+
+
+def test_k4_full_geometry_candidates_match_oracle(tables_k4, ora):
+    """Config C (-k 4, default -n): 2^24 baby steps, 57.5 MiB level-1 bloom.  Every candidate of two
+    whole chunks (2 x 1024 groups) equals the oracle's, and the key comes back through the second
+    check at k = 4 (M3 = 16384)."""
+    from keyhuntm1cpu_amd.khbsgs import Engine
+    bs = ora.Bsgs(None, 4)
+    assert bs.m == tables_k4.m == 1 << 24 and bs.cycles == tables_k4.cycles == 1024
+    key = 0x2832ED74F2B5E35EE
+    t = ora.pubkey(key)
+    bases = [key - 987654321098, (1 << 65) + (9 << 45)]
+    with Engine(0) as e:
+        bf, nb, bits, h = tables_k4.bloom_concat(1)
+        e.load_bloom(bf, nb, bits, h)
+        e.load_giant_table(tables_k4.giant_table())
+        offs, gpl = tables_k4.lane_offsets()
+        e.load_lane_offsets(offs, gpl)
+        centres = b"".join(tables_k4.chunk_centre(b, t.be64()) for b in bases)
+        got, degen, st = e.scan(centres, 0, tables_k4.cycles)
+    assert not degen
+    for j, b in enumerate(bases):
+        ref, _, _ = bs.scan(bs.chunk_start(b, t), 0, bs.cycles)
+        assert sorted(a for jj, a in got if jj == j) == sorted(ref)
+    a_hits = [a for jj, a in got if jj == 0]
+    assert any(tables_k4.secondcheck(bases[0], a, t.be64()) == key for a in a_hits)
+
+
+def test_k4_synthetic_key_search(tables_k4):
+    """SURVEY.md §8d synthetic input for B/C: d = 2^65 + off, off from splitmix64 seeded
+    0x6b657968756e7466 (parity-sized: off < 2^47, found within 4 chunks), sequential from 2^65."""
+    off = next(_splitmix64(0x6B657968756E7466)) & ((1 << 47) - 1)
+    d = (1 << 65) + off
+    xy = khhost.pubkey(d)
+    res, st = tables_k4.search([xy], 1 << 65, (1 << 65) + (1 << 47))
+    assert res == [d]
+    assert st["chunks"] <= 4
