@@ -111,6 +111,37 @@ int khb_field_op(khb_ctx* ctx, int op, const uint8_t* a, const uint8_t* b, uint8
 /* Bloom self-test kernel: hit[i] = bloom_check(level-1, x[i]) for 32-byte BE x values. */
 int khb_probe(khb_ctx* ctx, const uint8_t* xs, uint8_t* hit, uint32_t n);
 
+/* ---- -m address / -m rmd160 (keyhunt.cpp:2586-2937, BTC P2PKH, no endomorphism) ----
+ * The same group walk with the table Gn[i] = (i+1)*stride*G, _2Gn = 1024*stride*G loaded through
+ * khb_load_giant_table (init_generator, keyhunt.cpp:4386-4399), lane offsets as above.  A job is
+ * one claimed chunk; centres[k] = pubkey(chunk_base_k + 512*stride) (keyhunt.cpp:2587-2589), so
+ * point t of group j of job k is the key chunk_base_k + (1024*j + t)*stride. */
+typedef struct {
+  uint32_t job;
+  uint32_t group;
+  uint32_t t;
+  uint32_t kind;     /* 0 = compressed prefix 02, 1 = compressed prefix 03, 2 = uncompressed */
+} khb_addr_hit;
+
+/* The single target bloom of -m address (bloom over 20-byte hash160 values, initBloomFilter,
+ * keyhunt.cpp:6559-6576). */
+int khb_load_addr_bloom(khb_ctx* ctx, const uint8_t* bf, uint64_t bytes, uint64_t bits, uint32_t hashes);
+/* search: 0 = uncompress, 1 = compress, 2 = both (keyhunt.cpp:59-61, -l).  Every point's hash160(s)
+ * are probed in the bloom; bloom hits are returned (the host runs searchbinary and the key
+ * recovery).  group_begin must be a multiple of groups_per_lane. */
+int khb_addr_submit(khb_ctx* ctx, const uint8_t* centres_xy_be, uint32_t n_jobs, uint32_t group_begin,
+                    uint32_t group_count, int search);
+/* stats->n_cand = number of bloom hits (may exceed cap); giant_steps = keys scanned. */
+int khb_addr_collect(khb_ctx* ctx, khb_addr_hit* hits, uint32_t cap, khb_stats* stats);
+int khb_addr_scan(khb_ctx* ctx, const uint8_t* centres_xy_be, uint32_t n_jobs, uint32_t group_begin,
+                  uint32_t group_count, int search, khb_addr_hit* hits, uint32_t cap, khb_stats* stats);
+/* parity: x||y (64 bytes BE per point, t = 0..1023 per group) of ONE job. */
+int khb_addr_dump(khb_ctx* ctx, const uint8_t* centre_xy_be, uint32_t group_begin, uint32_t group_count,
+                  uint8_t* xy);
+/* self-test: out[21*i] = hash160 (20 bytes) of point i (x||y BE) for kind 0/1/2, then one byte =
+ * bloom_check20 result against the loaded address bloom (0 when none is loaded). */
+int khb_hash160(khb_ctx* ctx, int kind, const uint8_t* xy_be, uint8_t* out, uint32_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -61,6 +61,30 @@ void khh_session_close(khh_session* s);
 int khh_pubkey(const uint8_t key_be[32], uint8_t out_xy[64]);
 int khh_parse_pubkey(const char* hex, uint8_t out_xy[64], int* compressed);
 
+/* ---- -m address / -m rmd160 (BTC P2PKH) ----
+ * Targets from a target file's text (base58 addresses or 40-hex rmd160 lines, keyhunt.cpp:6300-6358).
+ * The generator (Gn table + lane offsets for chunks of n_seq keys) is built for stride and gpl. */
+typedef struct khh_addr khh_addr;
+khh_addr* khh_addr_new(const char* text, int bloom_multiplier, const uint8_t stride_be[32], uint64_t n_seq,
+                       uint32_t gpl, int threads, char* err, size_t errlen);
+void khh_addr_free(khh_addr* a);
+/* sorted 20-byte table (n entries) and the target bloom */
+const uint8_t* khh_addr_table(const khh_addr* a, uint64_t* n);
+const uint8_t* khh_addr_bloom(const khh_addr* a, uint64_t* bytes, uint64_t* bits, uint32_t* hashes);
+void khh_addr_giant_table(const khh_addr* a, uint8_t out[513 * 64]);
+uint32_t khh_addr_lane_offsets(const khh_addr* a, uint8_t* out /* n*64, may be NULL */, uint32_t* gpl);
+/* Sequential (random_chunks = 0) or -R search of [start, end) with search 0/1/2 (-l).  Found keys
+ * (32 B BE each) with compressed flags and rmd160s, in discovery order; *n_found may exceed cap.
+ * stats_out (nullable, 6): [0]=chunks [1]=keys [2]=bloom hits [3]=degenerate groups [4]=kernel us
+ * [5]=launches. */
+int khh_addr_search(const khh_addr* a, const uint8_t start_be[32], const uint8_t end_be[32], int search,
+                    int random_chunks, const int* devices, int n_devices, uint32_t lanes, uint64_t max_chunks,
+                    uint8_t* keys_be, uint8_t* compressed, uint8_t* rmd, uint32_t cap, uint32_t* n_found,
+                    uint64_t* stats_out, char* err, size_t errlen);
+/* hash160 of a public key (x||y BE) and its P2PKH address (out_addr >= 36 bytes) */
+void khh_hash160(const uint8_t xy[64], int compressed, uint8_t out[20]);
+void khh_rmd_to_address(const uint8_t rmd[20], char* out_addr);
+
 #ifdef __cplusplus
 }
 #endif

@@ -95,9 +95,8 @@ KHB_HD const uint8_t* sub_bloom(const uint8_t* __restrict__ bf_all, const BloomG
 // b = XXH64(x, seed = a), bit i at (a + b*i) mod bits.  R bit positions are fetched per round
 // (independent loads, one memory round trip); the result is the same AND of all bits for any R.
 template <int R>
-KHB_HD bool bloom_rest_r(const uint8_t* __restrict__ bf, const BloomGeom& g, const uint64_t w[4], uint64_t a) {
+KHB_HD bool bloom_steps(const uint8_t* __restrict__ bf, const BloomGeom& g, uint64_t a, uint64_t b) {
   uint64_t pos = mod_bits(a, g);
-  const uint64_t b = xxh64_32(w, a);
   const uint64_t bm = mod_bits(b, g);
   uint64_t h = a;
   for (uint32_t i = 1; i < g.hashes; i += R) {
@@ -118,6 +117,11 @@ KHB_HD bool bloom_rest_r(const uint8_t* __restrict__ bf, const BloomGeom& g, con
     if (!ok) return false;
   }
   return true;
+}
+
+template <int R>
+KHB_HD bool bloom_rest_r(const uint8_t* __restrict__ bf, const BloomGeom& g, const uint64_t w[4], uint64_t a) {
+  return bloom_steps<R>(bf, g, a, xxh64_32(w, a));
 }
 
 // bloom_rest for two independent x at once (ok1/ok2 in: entry valid, out: all bits set).  Each

@@ -1,0 +1,456 @@
+#include "address_host.hpp"
+
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <thread>
+
+#include "../../../include/khbsgs.h"
+#include "../device/hash160.hpp"
+
+namespace khb {
+
+// ------------------------------------------------------------------------------- hashing
+void sha256(const uint8_t* msg, size_t len, uint8_t out[32]) {
+  uint32_t s[8], w[16];
+  sha256_init(s);
+  uint8_t blk[128];
+  size_t i = 0;
+  auto load = [&](const uint8_t* b) {
+    for (int k = 0; k < 16; ++k)
+      w[k] = ((uint32_t)b[4 * k] << 24) | ((uint32_t)b[4 * k + 1] << 16) | ((uint32_t)b[4 * k + 2] << 8) | b[4 * k + 3];
+  };
+  for (; i + 64 <= len; i += 64) {
+    load(msg + i);
+    sha256_block(s, w);
+  }
+  const size_t rem = len - i;
+  memset(blk, 0, sizeof blk);
+  memcpy(blk, msg + i, rem);
+  blk[rem] = 0x80;
+  const size_t total = rem >= 56 ? 128 : 64;
+  const uint64_t bits = (uint64_t)len * 8;
+  for (int k = 0; k < 8; ++k) blk[total - 1 - k] = (uint8_t)(bits >> (8 * k));
+  for (size_t o = 0; o < total; o += 64) {
+    load(blk + o);
+    sha256_block(s, w);
+  }
+  for (int k = 0; k < 8; ++k) {
+    out[4 * k] = (uint8_t)(s[k] >> 24); out[4 * k + 1] = (uint8_t)(s[k] >> 16);
+    out[4 * k + 2] = (uint8_t)(s[k] >> 8); out[4 * k + 3] = (uint8_t)s[k];
+  }
+}
+
+static void fe_of_pt(Fe& x, Fe& y, const Pt& p) {
+  uint8_t b[64];
+  pt_to_be(b, p);
+  fe_from_be(x, b);
+  fe_from_be(y, b + 32);
+}
+
+static void bytes_of_words(uint8_t out[20], const uint32_t h[5]) {
+  for (int k = 0; k < 5; ++k)
+    for (int b = 0; b < 4; ++b) out[4 * k + b] = (uint8_t)(h[k] >> (8 * b));
+}
+
+void hash160_pub(const Pt& p, bool compressed, uint8_t out[20]) {
+  Fe x, y;
+  fe_of_pt(x, y, p);
+  uint32_t h[5];
+  if (compressed)
+    hash160_compressed(h, (y.v[0] & 1) ? 3u : 2u, x);
+  else
+    hash160_uncompressed(h, x, y);
+  bytes_of_words(out, h);
+}
+
+void hash160_x(uint8_t prefix, const Pt& p, uint8_t out[20]) {
+  Fe x, y;
+  fe_of_pt(x, y, p);
+  uint32_t h[5];
+  hash160_compressed(h, prefix, x);
+  bytes_of_words(out, h);
+}
+
+// -------------------------------------------------------------------------------- base58
+static const char kB58[] = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz";
+
+static int b58_digit(unsigned char c) {
+  if (!c || (c & 0x80)) return -1;
+  const char* p = strchr(kB58, c);
+  return p ? (int)(p - kB58) : -1;
+}
+
+bool b58decode25(const char* s, uint8_t out[25]) {
+  const size_t n = strlen(s);
+  size_t i = 0, zeros = 0;
+  memset(out, 0, 25);
+  for (; i < n && s[i] == '1'; ++i) ++zeros;
+  for (; i < n; ++i) {
+    const int v = b58_digit((unsigned char)s[i]);
+    if (v < 0) return false;
+    uint32_t carry = (uint32_t)v;
+    for (int k = 24; k >= 0; --k) {
+      const uint32_t t = (uint32_t)out[k] * 58u + carry;
+      out[k] = (uint8_t)t;
+      carry = t >> 8;
+    }
+    if (carry) return false;   // "Output number too big"
+  }
+  size_t lz = 0;
+  while (lz < 25 && out[lz] == 0) ++lz;
+  return 25 - lz + zeros == 25;  // keyhunt.cpp:6338: raw_value_length == 25
+}
+
+std::string rmd_to_address(const uint8_t rmd[20]) {
+  uint8_t d[25], h1[32], h2[32];
+  d[0] = 0x00;   // byte_encode_crypto (P2PKH)
+  memcpy(d + 1, rmd, 20);
+  sha256(d, 21, h1);
+  sha256(h1, 32, h2);
+  memcpy(d + 21, h2, 4);
+  size_t zc = 0;
+  while (zc < 25 && !d[zc]) ++zc;
+  const size_t size = (25 - zc) * 138 / 100 + 1;   // b58enc (base58.c:145-189)
+  std::vector<uint8_t> buf(size, 0);
+  size_t high = size - 1, j = 0;
+  for (size_t i = zc; i < 25; ++i, high = j) {
+    int carry = d[i];
+    for (j = size - 1; (j > high) || carry; --j) {
+      carry += 256 * buf[j];
+      buf[j] = (uint8_t)(carry % 58);
+      carry /= 58;
+      if (!j) break;
+    }
+  }
+  for (j = 0; j < size && !buf[j]; ++j) {}
+  std::string out(zc, '1');
+  for (; j < size; ++j) out += kB58[buf[j]];
+  return out;
+}
+
+// ------------------------------------------------------------------------------- targets
+static void trim(char* s) {
+  const char* seps = " \t\n\r";
+  size_t n = strlen(s);
+  while (n && strchr(seps, s[n - 1])) s[--n] = 0;
+  const size_t k = strspn(s, seps);
+  if (k) memmove(s, s + k, n + 1 - k);
+}
+
+static bool all_b58(const char* s) {
+  for (; *s; ++s)
+    if (b58_digit((unsigned char)*s) < 0) return false;
+  return true;
+}
+
+static bool all_hex(const char* s) {
+  for (; *s; ++s) {
+    const char c = *s;
+    if (!((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'))) return false;
+  }
+  return true;
+}
+
+static int hexv(char c) { return c <= '9' ? c - '0' : (c | 32) - 'a' + 10; }
+
+// Split like fgets(aux, 100, f): a line longer than 99 characters continues in the next read.
+static std::vector<std::string> fgets_lines(const std::string& text) {
+  std::vector<std::string> out;
+  size_t p = 0;
+  while (p < text.size()) {
+    size_t e = text.find('\n', p);
+    size_t len = (e == std::string::npos ? text.size() : e + 1) - p;
+    if (len > 99) len = 99;
+    out.push_back(text.substr(p, len));
+    p += len;
+  }
+  return out;
+}
+
+bool AddrTargets::load_text(const std::string& text, int bloom_multiplier, AddrTargets& T, std::string* err) {
+  T = AddrTargets();
+  const std::vector<std::string> lines = fgets_lines(text);
+  char aux[128];
+  for (const std::string& l : lines) {
+    snprintf(aux, sizeof aux, "%s", l.c_str());
+    trim(aux);
+    if (strlen(aux) > 20) ++T.counted;
+  }
+  // initBloomFilter (keyhunt.cpp:6559-6576)
+  const uint64_t entries = T.counted <= 10000 ? 10000 : (uint64_t)(bloom_multiplier > 0 ? bloom_multiplier : 1) * T.counted;
+  if (T.bloom.init2(entries, 0.000001L) != 0) {
+    if (err) *err = "bloom_init failed";
+    return false;
+  }
+  uint64_t items = T.counted, i = 0;
+  size_t li = 0;
+  while (i < items && li < lines.size()) {
+    snprintf(aux, sizeof aux, "%s", lines[li++].c_str());
+    trim(aux);
+    const size_t r = strlen(aux);
+    bool valid = false;
+    if (r > 0 && r <= 40) {
+      if (r < 40 && all_b58(aux)) {
+        uint8_t raw[25];
+        if (b58decode25(aux, raw)) {
+          H160 h;
+          memcpy(h.data(), raw + 1, 20);
+          T.bloom.add20(h.data());
+          T.table.push_back(h);
+          ++i;
+          valid = true;
+        }
+      }
+      if (r == 40 && all_hex(aux)) {
+        H160 h;
+        for (int k = 0; k < 20; ++k) h[k] = (uint8_t)(hexv(aux[2 * k]) * 16 + hexv(aux[2 * k + 1]));
+        T.bloom.add20(h.data());
+        T.table.push_back(h);
+        ++i;
+        valid = true;
+      }
+    }
+    if (!valid) {
+      T.skipped.push_back(aux);
+      --items;
+    }
+  }
+  std::sort(T.table.begin(), T.table.end(),
+            [](const H160& a, const H160& b) { return memcmp(a.data(), b.data(), 20) < 0; });
+  return true;
+}
+
+bool AddrTargets::load_file(const char* path, int bloom_multiplier, AddrTargets& T, std::string* err) {
+  FILE* f = fopen(path, "r");
+  if (!f) {
+    if (err) *err = std::string("Error opening the file ") + path;
+    return false;
+  }
+  std::string text;
+  char buf[65536];
+  size_t n;
+  while ((n = fread(buf, 1, sizeof buf, f)) > 0) text.append(buf, n);
+  fclose(f);
+  return load_text(text, bloom_multiplier, T, err);
+}
+
+bool AddrTargets::searchbinary(const uint8_t data[20]) const {
+  int64_t half, min = 0, max = (int64_t)table.size(), current = 0;
+  bool r = false;
+  half = max;
+  while (!r && half >= 1) {
+    half = (max - min) / 2;
+    const int rcmp = memcmp(data, table[(size_t)(current + half)].data(), 20);
+    if (rcmp == 0) {
+      r = true;
+    } else {
+      if (rcmp < 0) max = max - half;
+      else min = min + half;
+      current = min;
+    }
+  }
+  return r;
+}
+
+// ----------------------------------------------------------------------------- generator
+void AddrGen::build(const U256& s, uint32_t groups_per_chunk, uint32_t g_per_lane, int threads) {
+  stride = s;
+  gpl = g_per_lane;
+  gn.assign(513, Pt());
+  const Pt G = mul_g(stride);
+  gn[0] = G;
+  gn[1] = double_direct(G);
+  for (int i = 2; i < 512; ++i) gn[i] = add_direct(gn[i - 1], G);
+  gn[512] = double_direct(gn[511]);
+  const uint32_t n_off = (groups_per_chunk + gpl - 1) / gpl;
+  offs.assign(n_off ? n_off : 1, Pt());
+  std::atomic<uint32_t> next{1};
+  auto work = [&] {
+    for (;;) {
+      const uint32_t m = next.fetch_add(1);
+      if (m >= n_off) break;
+      U256 k = stride * ((uint64_t)m * gpl * 1024u), r;
+      U256::divmod(k, secp_order(), nullptr, &r);
+      offs[m] = r.is_zero() ? Pt() : mul_g(r);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; ++t) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+}
+
+std::vector<uint8_t> AddrGen::table_be() const {
+  std::vector<uint8_t> out(64 * gn.size());
+  for (size_t i = 0; i < gn.size(); ++i) pt_to_be(out.data() + 64 * i, gn[i]);
+  return out;
+}
+
+std::vector<uint8_t> AddrGen::offs_be() const {
+  std::vector<uint8_t> out(64 * offs.size());
+  for (size_t i = 0; i < offs.size(); ++i) pt_to_be(out.data() + 64 * i, offs[i]);
+  return out;
+}
+
+// -------------------------------------------------------------------------------- search
+namespace {
+
+struct AddrShared {
+  const AddrTargets& T;
+  const AddrGen& G;
+  const AddrConfig& cfg;
+  const AddrCallbacks& cb;
+  U256 cursor;
+  uint64_t claimed = 0;
+  std::mutex mu;
+  AddrStats& stats;
+  std::string err;
+  int rc = 0;
+};
+
+// Confirm one GPU bloom hit on the host: searchbinary, then the reference's key recovery.
+bool confirm_hit(const AddrTargets& T, const U256& key, uint32_t kind, AddrFound* out) {
+  U256 k;
+  U256::divmod(key, secp_order(), nullptr, &k);
+  if (k.is_zero()) return false;
+  const Pt P = mul_g(k);
+  uint8_t h[20];
+  if (kind < 2) {
+    hash160_x((uint8_t)(2 + kind), P, h);
+    if (!T.searchbinary(h)) return false;
+    uint8_t hc[20];
+    hash160_pub(P, true, hc);
+    // keyhunt.cpp:2811-2822: the x-only hit belongs to k or to n - k
+    out->key = memcmp(h, hc, 20) != 0 ? secp_order() - key : key;
+    out->compressed = true;
+  } else {
+    hash160_pub(P, false, h);
+    if (!T.searchbinary(h)) return false;
+    out->key = key;
+    out->compressed = false;
+  }
+  memcpy(out->rmd.data(), h, 20);
+  return true;
+}
+
+void device_loop(AddrShared& S, int device) {
+  khb_ctx* ctx = nullptr;
+  int rc = khb_open(device, S.cfg.lanes, &ctx);
+  auto fail = [&](int code, const char* what) {
+    std::lock_guard<std::mutex> lk(S.mu);
+    if (!S.rc) {
+      S.rc = code;
+      S.err = std::string(what) + ": " + khb_strerror(code);
+    }
+  };
+  if (rc) return fail(rc, "khb_open");
+  const uint32_t groups = (uint32_t)(S.cfg.n_seq / 1024);
+  const std::vector<uint8_t> gtab = S.G.table_be(), offs = S.G.offs_be();
+  const BloomGeom bg = S.T.bloom.geom();
+  if ((rc = khb_load_giant_table(ctx, gtab.data())) ||
+      (rc = khb_load_lane_offsets(ctx, offs.data(), (uint32_t)S.G.offs.size(), S.G.gpl)) ||
+      (rc = khb_load_addr_bloom(ctx, S.T.bloom.bf.data(), bg.bytes_per_sub, bg.bits, bg.hashes))) {
+    khb_close(ctx);
+    return fail(rc, "table upload");
+  }
+  const uint64_t lanes_per_job = (groups + S.G.gpl - 1) / S.G.gpl;
+  const uint64_t lanes = khb_lanes(ctx);
+  uint64_t per_batch = (2 * lanes + lanes_per_job - 1) / lanes_per_job;
+  if (per_batch < 1) per_batch = 1;
+  if (per_batch > 4096) per_batch = 4096;
+  std::vector<khb_addr_hit> hits(1u << 18);
+  const U256 half = S.G.stride * 512u;
+  for (;;) {
+    if (S.cb.stop && S.cb.stop()) break;
+    std::vector<U256> bases;
+    {
+      std::lock_guard<std::mutex> lk(S.mu);
+      if (S.rc) break;
+      while (bases.size() < per_batch) {
+        if (S.cfg.max_chunks && S.claimed >= S.cfg.max_chunks) break;
+        if (S.cfg.random) {
+          bases.push_back(random_in(S.cfg.start, S.cfg.end));
+        } else {
+          if (!(S.cursor < S.cfg.end)) break;
+          bases.push_back(S.cursor);
+          S.cursor = S.cursor + U256(S.cfg.n_seq);
+        }
+        ++S.claimed;
+      }
+    }
+    if (bases.empty()) break;
+    if (S.cb.on_chunk)
+      for (const U256& b : bases) S.cb.on_chunk(b, device);
+    std::vector<uint8_t> centres(64 * bases.size());
+    for (size_t k = 0; k < bases.size(); ++k) {
+      U256 c = bases[k] + half, r;   // startP = ComputePublicKey(key_mpz + 512*stride)
+      U256::divmod(c, secp_order(), nullptr, &r);
+      pt_to_be(centres.data() + 64 * k, mul_g(r));
+    }
+    khb_stats st{};
+    rc = khb_addr_scan(ctx, centres.data(), (uint32_t)bases.size(), 0, groups, S.cfg.search, hits.data(),
+                       (uint32_t)hits.size(), &st);
+    if (rc) {
+      fail(rc, "khb_addr_scan");
+      break;
+    }
+    const uint32_t nh = st.n_cand < hits.size() ? st.n_cand : (uint32_t)hits.size();
+    std::sort(hits.begin(), hits.begin() + nh, [](const khb_addr_hit& a, const khb_addr_hit& b) {
+      if (a.job != b.job) return a.job < b.job;
+      if (a.group != b.group) return a.group < b.group;
+      if (a.t != b.t) return a.t < b.t;
+      return a.kind < b.kind;
+    });
+    std::vector<AddrFound> found;
+    for (uint32_t i = 0; i < nh; ++i) {
+      const khb_addr_hit& h = hits[i];
+      const U256 key = bases[h.job] + S.G.stride * ((uint64_t)h.group * 1024u + h.t);
+      AddrFound f;
+      if (confirm_hit(S.T, key, h.kind, &f)) found.push_back(f);
+    }
+    std::lock_guard<std::mutex> lk(S.mu);
+    S.stats.launches++;
+    S.stats.chunks += bases.size();
+    S.stats.keys += st.giant_steps;
+    S.stats.hits += st.n_cand;
+    S.stats.degenerate += st.n_degenerate;
+    S.stats.kernel_seconds += st.kernel_ms * 1e-3;
+    S.stats.found += found.size();
+    if (S.cb.on_found)
+      for (const AddrFound& f : found) S.cb.on_found(f);
+    if (st.n_cand > hits.size() && !S.rc) {
+      S.rc = -100;
+      S.err = "bloom hit buffer overflow (target bloom too full for this batch)";
+    }
+  }
+  khb_close(ctx);
+}
+
+}  // namespace
+
+int addr_search(const AddrTargets& T, const AddrGen& G, const AddrConfig& cfg, const AddrCallbacks& cb,
+                AddrStats* stats, std::string* err) {
+  AddrStats local;
+  AddrStats& st = stats ? *stats : local;
+  st = AddrStats();
+  if (cfg.n_seq < 1024 || cfg.n_seq % 1024 || cfg.n_seq / 1024 > 0xFFFFFFFFull) {
+    if (err) *err = "n must be a positive multiple of 1024";
+    return -100;
+  }
+  if ((cfg.n_seq / 1024 + G.gpl - 1) / G.gpl > G.offs.size()) {
+    if (err) *err = "generator lane offsets do not cover a chunk";
+    return -100;
+  }
+  AddrShared S{T, G, cfg, cb, cfg.start, 0, {}, st, {}, 0};
+  std::vector<std::thread> th;
+  for (int d : cfg.devices) th.emplace_back(device_loop, std::ref(S), d);
+  for (auto& t : th) t.join();
+  if (S.rc && err) *err = S.err;
+  return S.rc;
+}
+
+}  // namespace khb

@@ -1,4 +1,5 @@
 #include "bloom_host.hpp"
+#include "../device/hash160.hpp"
 
 #include <math.h>
 #include <string.h>
@@ -58,6 +59,33 @@ void BloomFilter::add32_atomic(const uint8_t x[32]) {
     const uint64_t pos = (a + b * i) % bits;
     const uint8_t m = (uint8_t)(1u << (pos & 7));
     if (!(__atomic_load_n(&base[pos >> 3], __ATOMIC_RELAXED) & m)) __atomic_fetch_or(&base[pos >> 3], m, __ATOMIC_RELAXED);
+  }
+}
+
+static void words_of_bytes20(uint32_t h[5], const uint8_t b[20]) {
+  for (int k = 0; k < 5; ++k) memcpy(&h[k], b + 4 * k, 4);   // little-endian host
+}
+
+bool BloomFilter::check20(const uint8_t hb[20]) const {
+  uint32_t h[5];
+  words_of_bytes20(h, hb);
+  const uint64_t a = xxh64_20(h, KHB_BLOOM_SEED);
+  const uint64_t b = xxh64_20(h, a);
+  for (uint32_t i = 0; i < hashes; ++i) {
+    const uint64_t pos = (a + b * i) % bits;
+    if (!((bf[pos >> 3] >> (pos & 7)) & 1)) return false;
+  }
+  return true;
+}
+
+void BloomFilter::add20(const uint8_t hb[20]) {
+  uint32_t h[5];
+  words_of_bytes20(h, hb);
+  const uint64_t a = xxh64_20(h, KHB_BLOOM_SEED);
+  const uint64_t b = xxh64_20(h, a);
+  for (uint32_t i = 0; i < hashes; ++i) {
+    const uint64_t pos = (a + b * i) % bits;
+    bf[pos >> 3] |= (uint8_t)(1u << (pos & 7));
   }
 }
 

@@ -36,17 +36,6 @@ void parallel_for(size_t n, int threads, F&& fn) {
   for (auto& t : th) t.join();
 }
 
-// Uniform random value in [lo, hi) (the -B random chunk policy; Int::Rand, Int.cpp:751-765).
-U256 random_in(const U256& lo, const U256& hi) {
-  U256 span = hi - lo, v, r;
-  uint8_t b[32];
-  if (getrandom(b, sizeof b, 0) != (ssize_t)sizeof b) memset(b, 0x5a, sizeof b);
-  v = U256::from_be(b);
-  if (span.is_zero()) return lo;
-  U256::divmod(v, span, nullptr, &r);
-  return lo + r;
-}
-
 struct Shared {
   const Tables& T;
   const std::vector<Target>& targets;

@@ -6,6 +6,7 @@
 
 #include "../../../include/khbsgs.h"
 #include "../../../include/khhost.h"
+#include "address_host.hpp"
 #include "bsgs_host.hpp"
 #include "engine.hpp"
 
@@ -13,6 +14,12 @@ using namespace khb;
 
 struct khh_tables {
   Tables t;
+};
+
+struct khh_addr {
+  AddrTargets T;
+  AddrGen G;
+  uint64_t n_seq = 0;
 };
 
 static void set_err(char* err, size_t n, const std::string& m) {
@@ -177,6 +184,111 @@ int khh_parse_pubkey(const char* hex, uint8_t out_xy[64], int* compressed) {
   pt_to_be(out_xy, p);
   if (compressed) *compressed = c ? 1 : 0;
   return 0;
+}
+
+khh_addr* khh_addr_new(const char* text, int bloom_multiplier, const uint8_t stride_be[32], uint64_t n_seq,
+                       uint32_t gpl, int threads, char* err, size_t errlen) {
+  if (!text || n_seq < 1024 || n_seq % 1024) {
+    set_err(err, errlen, "n must be a positive multiple of 1024");
+    return nullptr;
+  }
+  khh_addr* a = new khh_addr();
+  std::string e;
+  if (!AddrTargets::load_text(text, bloom_multiplier, a->T, &e)) {
+    set_err(err, errlen, e);
+    delete a;
+    return nullptr;
+  }
+  const U256 stride = stride_be ? U256::from_be(stride_be) : U256(1);
+  if (stride.is_zero()) {
+    set_err(err, errlen, "stride must be positive");
+    delete a;
+    return nullptr;
+  }
+  if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
+  a->n_seq = n_seq;
+  a->G.build(stride, (uint32_t)(n_seq / 1024), gpl ? gpl : 16, threads);
+  return a;
+}
+
+void khh_addr_free(khh_addr* a) { delete a; }
+
+const uint8_t* khh_addr_table(const khh_addr* a, uint64_t* n) {
+  if (n) *n = a->T.table.size();
+  return a->T.table.empty() ? nullptr : a->T.table[0].data();
+}
+
+const uint8_t* khh_addr_bloom(const khh_addr* a, uint64_t* bytes, uint64_t* bits, uint32_t* hashes) {
+  if (bytes) *bytes = a->T.bloom.bytes;
+  if (bits) *bits = a->T.bloom.bits;
+  if (hashes) *hashes = a->T.bloom.hashes;
+  return a->T.bloom.bf.data();
+}
+
+void khh_addr_giant_table(const khh_addr* a, uint8_t out[513 * 64]) {
+  const std::vector<uint8_t> v = a->G.table_be();
+  memcpy(out, v.data(), v.size());
+}
+
+uint32_t khh_addr_lane_offsets(const khh_addr* a, uint8_t* out, uint32_t* gpl) {
+  if (gpl) *gpl = a->G.gpl;
+  if (out) {
+    const std::vector<uint8_t> v = a->G.offs_be();
+    memcpy(out, v.data(), v.size());
+  }
+  return (uint32_t)a->G.offs.size();
+}
+
+int khh_addr_search(const khh_addr* a, const uint8_t start_be[32], const uint8_t end_be[32], int search,
+                    int random_chunks, const int* devices, int n_devices, uint32_t lanes, uint64_t max_chunks,
+                    uint8_t* keys_be, uint8_t* compressed, uint8_t* rmd, uint32_t cap, uint32_t* n_found,
+                    uint64_t* stats_out, char* err, size_t errlen) {
+  if (!a || !start_be || !end_be || search < 0 || search > 2) return KHB_EINVAL;
+  AddrConfig cfg;
+  cfg.search = search;
+  cfg.start = U256::from_be(start_be);
+  cfg.end = U256::from_be(end_be);
+  cfg.n_seq = a->n_seq;
+  cfg.random = random_chunks != 0;
+  cfg.lanes = lanes;
+  cfg.gpl = a->G.gpl;
+  cfg.max_chunks = max_chunks;
+  cfg.devices.clear();
+  for (int i = 0; i < n_devices; ++i) cfg.devices.push_back(devices[i]);
+  if (cfg.devices.empty()) cfg.devices.push_back(0);
+  uint32_t nf = 0;
+  AddrCallbacks cb;
+  cb.on_found = [&](const AddrFound& f) {
+    if (nf < cap) {
+      if (keys_be) f.key.to_be(keys_be + 32 * (size_t)nf);
+      if (compressed) compressed[nf] = f.compressed ? 1 : 0;
+      if (rmd) memcpy(rmd + 20 * (size_t)nf, f.rmd.data(), 20);
+    }
+    ++nf;
+  };
+  AddrStats st;
+  std::string e;
+  const int rc = addr_search(a->T, a->G, cfg, cb, &st, &e);
+  if (n_found) *n_found = nf;
+  if (stats_out) {
+    stats_out[0] = st.chunks;
+    stats_out[1] = st.keys;
+    stats_out[2] = st.hits;
+    stats_out[3] = st.degenerate;
+    stats_out[4] = (uint64_t)(st.kernel_seconds * 1e6);
+    stats_out[5] = st.launches;
+  }
+  if (rc) set_err(err, errlen, e);
+  return rc;
+}
+
+void khh_hash160(const uint8_t xy[64], int compressed, uint8_t out[20]) {
+  hash160_pub(pt_from_be(xy), compressed != 0, out);
+}
+
+void khh_rmd_to_address(const uint8_t rmd[20], char* out_addr) {
+  const std::string s = rmd_to_address(rmd);
+  memcpy(out_addr, s.c_str(), s.size() + 1);
 }
 
 }  // extern "C"

@@ -1,6 +1,7 @@
 #include "u256.hpp"
 
 #include <string.h>
+#include <sys/random.h>
 
 namespace khb {
 
@@ -171,6 +172,16 @@ U256 U256::from_be(const uint8_t in[32]) {
     r.w[i] = v;
   }
   return r;
+}
+
+U256 random_in(const U256& lo, const U256& hi) {
+  U256 span = hi - lo, v, r;
+  uint8_t b[32];
+  if (getrandom(b, sizeof b, 0) != (ssize_t)sizeof b) memset(b, 0x5a, sizeof b);
+  v = U256::from_be(b);
+  if (span.is_zero()) return lo;
+  U256::divmod(v, span, nullptr, &r);
+  return lo + r;
 }
 
 }  // namespace khb

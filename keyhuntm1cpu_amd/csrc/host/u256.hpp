@@ -46,4 +46,8 @@ struct U256 {
   static U256 from_be(const uint8_t in[32]);
 };
 
+// Uniform random value in [lo, hi) from getrandom (Int::Rand, Int.cpp:751-765 / Random.cpp:133-145:
+// the -R / -B random policies, non-deterministic like the reference's).
+U256 random_in(const U256& lo, const U256& hi);
+
 }  // namespace khb

@@ -21,6 +21,7 @@
 #include "device/fe.hpp"
 #include "device/fe_asm.hpp"
 #include "device/bloom_probe.hpp"
+#include "device/hash160.hpp"
 
 using namespace khb;
 
@@ -43,8 +44,22 @@ struct AffPt {
 #define KHB_WAVES_PER_SIMD 4      // occupancy target of k_giant_scan (launch bounds); w4 measured best
 #endif
 constexpr uint32_t kBlock = 256;
+
+// Kernel modes (template argument of scan_group / k_giant_scan).
+enum : int {
+  kScan = 0,       // -m bsgs: level-1 bloom probe of every x
+  kDump = 1,       // -m bsgs parity: write every x
+  kAddrU = 2,      // -m address, -l uncompress   (2 + keyhunt SEARCH_UNCOMPRESS, keyhunt.cpp:59-61)
+  kAddrC = 3,      // -m address, -l compress
+  kAddrB = 4,      // -m address, -l both (the reference default, keyhunt.cpp:300)
+  kAddrDump = 5,   // -m address parity: write every x||y
+};
+constexpr bool is_addr(int m) { return m >= kAddrU; }
+constexpr bool needs_y(int m) { return m == kAddrU || m == kAddrB || m == kAddrDump; }
+constexpr bool is_dump(int m) { return m == kDump || m == kAddrDump; }
 constexpr uint32_t kHalf = KHB_GROUP / 2;            // 512
 constexpr uint32_t kCandCap = 1u << 20;
+constexpr uint32_t kAddrHitCap = 1u << 18;
 constexpr uint32_t kDegenCap = 4096;
 
 struct ScanArgs {
@@ -57,7 +72,9 @@ struct ScanArgs {
   khb_cand* __restrict__ cand;
   khb_degenerate* __restrict__ degen;
   uint32_t* __restrict__ counters;     // [0] candidates [1] degenerate groups
-  uint8_t* __restrict__ xdump;         // DUMP builds only
+  uint8_t* __restrict__ xdump;         // dump modes only
+  uint32_t* __restrict__ ahits;        // -m address hits: {job, group, t, kind} x ahit_cap
+  uint32_t ahit_cap;
   uint64_t n_items;
   uint32_t n_jobs, group_begin, group_end, gpl, lanes_per_job, stride, cand_cap, degen_cap;
 };
@@ -243,12 +260,49 @@ struct GsnTable {
 #endif
 };
 
-// One reference group (keyhunt.cpp:3873-3999) centred on C; advances C to the next centre.
-// C is canonical on entry and exit; products are lazy (< 2^256) and every x is canonicalised
-// before it is hashed or dumped (fe_asm.hpp value contract).
-template <bool DUMP>
+// -m address handling of one point (keyhunt.cpp:2716-2937, BTC, no endomorphism): hash160 of
+// the compressed key for both prefixes from x alone (covers +k and -k, keyhunt.cpp:2719-2733) and/or
+// of the uncompressed key, each probed in the single target bloom; hits go to the host, which runs
+// searchbinary and the key recovery.  x and y are canonical.
+template <int MODE>
+__device__ __forceinline__ void addr_point(const ScanArgs& A, const Fe& x, const Fe& y, uint32_t job, uint32_t j,
+                                           uint32_t t) {
+  if constexpr (MODE == kAddrDump) {
+    uint8_t* o = A.xdump + ((uint64_t)(j - A.group_begin) * KHB_GROUP + t) * 64;
+    fe_to_be(o, x);
+    fe_to_be(o + 32, y);
+  } else {
+    uint32_t h[5];
+    auto emit = [&](uint32_t kind) {
+      const uint32_t k = atomicAdd(&A.counters[0], 1u);
+      if (k < A.ahit_cap) {
+        uint32_t* o = A.ahits + 4 * (size_t)k;
+        o[0] = job; o[1] = j; o[2] = t; o[3] = kind;
+      }
+    };
+    if constexpr (MODE == kAddrC || MODE == kAddrB) {
+#pragma unroll 1
+      for (uint32_t pre = 2; pre <= 3; ++pre) {
+        hash160_compressed(h, pre, x);
+        if (bloom_check20(A.bloom, A.geom, h)) emit(pre - 2);
+      }
+    }
+    if constexpr (MODE == kAddrU || MODE == kAddrB) {
+      hash160_uncompressed(h, x, y);
+      if (bloom_check20(A.bloom, A.geom, h)) emit(2);
+    }
+  }
+}
+
+// One reference group centred on C; advances C to the next centre.  For -m bsgs this is
+// keyhunt.cpp:3873-3999 (table GSn, x only); for -m address it is keyhunt.cpp:2586-2711 with the
+// table Gn (same point order t = 0..1023, pts[t] = key + t), plus y where the search needs it.
+// C is canonical on entry and exit; products are lazy (< 2^256) and every x (and y) is
+// canonicalised before it is hashed or dumped (fe_asm.hpp value contract).
+template <int MODE>
 __device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, AffPt& C, uint32_t job, uint32_t j,
                                            Fe* scr) {
+  constexpr bool DUMP = MODE == kDump;
   const uint32_t S = A.stride;
   // GSn rows are wave-uniform: read them through the constant address space so they arrive by
   // scalar loads (SGPRs, lgkmcnt) instead of occupying 16 VGPRs and the vector-memory queue.
@@ -299,29 +353,54 @@ __device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, Aff
     } else {
       idx = inv;
     }
-    Fe u, s, x1;
+    Fe u, s, x1, y1;
     const AffPt g = gsn.pt(i);
     fm_add(u, C.x, g.x);                  // x = s^2 - (C.x + GSn.x)
-    // C - GSn[i]: s = (-GSn.y - C.y)/dx; only s^2 is needed
+    // C - GSn[i]: s = (-GSn.y - C.y)/dx; x needs only s^2, and with s' = -s = (GSn.y + C.y)/dx
+    // y = (GSn.x - x)*s + GSn.y = (x - GSn.x)*s' + GSn.y   (keyhunt.cpp:2628-2641)
     fm_add(s, g.y, C.y);
     fm_mul(s, s, idx);
     fm_sqr(x1, s);
     fm_sub(x1, x1, u);
     fm_canon(x1, x1);
+    if constexpr (needs_y(MODE)) {
+      Fe t;
+      fm_sub(t, x1, g.x);
+      fm_mul(t, t, s);
+      fm_canon(t, t);
+      fm_add(y1, t, g.y);
+    }
     if (i < (int)kHalf - 1) {
-      // C + GSn[i]: s = (GSn.y - C.y)/dx
-      Fe x2;
+      // C + GSn[i]: s = (GSn.y - C.y)/dx; y = (GSn.x - x)*s - GSn.y   (keyhunt.cpp:2611-2624)
+      Fe x2, y2;
       fm_sub(s, g.y, C.y);
       fm_mul(s, s, idx);
       fm_sqr(x2, s);
       fm_sub(x2, x2, u);
       fm_canon(x2, x2);
-      probe_pair<DUMP>(A, Q, x1, x2, job, j, kHalf - 1 - (uint32_t)i, kHalf + 1 + (uint32_t)i);
+      if constexpr (is_addr(MODE)) {
+        if constexpr (needs_y(MODE)) {
+          fm_sub(y2, g.x, x2);
+          fm_mul(y2, y2, s);
+          fm_sub(y2, y2, g.y);
+          fm_canon(y2, y2);
+        }
+        addr_point<MODE>(A, x1, y1, job, j, kHalf - 1 - (uint32_t)i);
+        addr_point<MODE>(A, x2, y2, job, j, kHalf + 1 + (uint32_t)i);
+      } else {
+        probe_pair<DUMP>(A, Q, x1, x2, job, j, kHalf - 1 - (uint32_t)i, kHalf + 1 + (uint32_t)i);
+      }
     } else {
-      probe<DUMP>(A, Q, x1, job, j, kHalf - 1 - (uint32_t)i);
+      if constexpr (is_addr(MODE))
+        addr_point<MODE>(A, x1, y1, job, j, kHalf - 1 - (uint32_t)i);
+      else
+        probe<DUMP>(A, Q, x1, job, j, kHalf - 1 - (uint32_t)i);
     }
   }
-  probe<DUMP>(A, Q, C.x, job, j, kHalf);
+  if constexpr (is_addr(MODE))
+    addr_point<MODE>(A, C.x, C.y, job, j, kHalf);
+  else
+    probe<DUMP>(A, Q, C.x, job, j, kHalf);
   // next centre: C + _2GSn with y (keyhunt.cpp:3986-3999)
   {
     asm volatile("" ::: "memory");
@@ -341,7 +420,7 @@ __device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, Aff
     C.x = nx;
     C.y = ny;
   }
-  if (!DUMP && degenerate) {
+  if (!is_dump(MODE) && degenerate) {
     uint32_t k = atomicAdd(&A.counters[1], 1u);
     if (k < A.degen_cap) A.degen[k] = khb_degenerate{job, j};
   }
@@ -368,15 +447,16 @@ __device__ __forceinline__ bool add_direct(AffPt& r, const AffPt& p1, const AffP
   return degenerate;
 }
 
-template <bool DUMP>
+template <int MODE>
 __global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanArgs A) {
+  constexpr bool QUEUE = MODE == kScan;
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   Fe* scr = A.scratch + lane;
-  __shared__ uint32_t s_queue[DUMP ? 1 : kWavesPerBlock][DUMP ? 1 : kQWords * kQCap];
+  __shared__ uint32_t s_queue[QUEUE ? kWavesPerBlock : 1][QUEUE ? kQWords * kQCap : 1];
   __shared__ uint32_t s_count[kWavesPerBlock];
-  const uint32_t wave = DUMP ? 0 : threadIdx.x >> 6;
+  const uint32_t wave = QUEUE ? threadIdx.x >> 6 : 0;
   ProbeQueue Q{s_queue[wave], &s_count[wave]};
-  if (!DUMP) *Q.n = 0;
+  if (QUEUE) *Q.n = 0;
   for (uint64_t item = lane; item < A.n_items; item += A.stride) {
     const uint32_t job = (uint32_t)(item / A.lanes_per_job);
     const uint32_t m = (uint32_t)(item % A.lanes_per_job);
@@ -385,14 +465,32 @@ __global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanA
     AffPt C = A.centres[job];
     const uint32_t mo = g0 / A.gpl;
     if (mo != 0) {
-      if (add_direct(C, C, A.offs[mo]) && !DUMP) {
+      if (add_direct(C, C, A.offs[mo]) && !is_dump(MODE)) {
         uint32_t k = atomicAdd(&A.counters[1], 1u);
         if (k < A.degen_cap) A.degen[k] = khb_degenerate{job, g0 | 0x80000000u};
       }
     }
-    for (uint32_t j = g0; j < g1; ++j) scan_group<DUMP>(A, Q, C, job, j, scr);
+    for (uint32_t j = g0; j < g1; ++j) scan_group<MODE>(A, Q, C, job, j, scr);
   }
-  if (!DUMP) q_drain(A, Q, 1);   // the wave has reconverged: finish what is still queued
+  if (QUEUE) q_drain(A, Q, 1);   // the wave has reconverged: finish what is still queued
+}
+
+// hash160 self-test: for x||y points, kind 0/1 = compressed with prefix 02/03, 2 = uncompressed;
+// out = 20 hash bytes + 1 byte bloom_check20 result (when a bloom is given).
+__global__ void k_hash160(const Fe* __restrict__ xy, int kind, const uint8_t* __restrict__ bloom, BloomGeom g,
+                          uint8_t* __restrict__ out, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Fe x = xy[2 * i], y = xy[2 * i + 1];
+  uint32_t h[5];
+  if (kind < 2)
+    hash160_compressed(h, 2u + (uint32_t)kind, x);
+  else
+    hash160_uncompressed(h, x, y);
+  uint8_t* o = out + 21 * (size_t)i;
+  for (int k = 0; k < 5; ++k)
+    for (int b = 0; b < 4; ++b) o[4 * k + b] = (uint8_t)(h[k] >> (8 * b));
+  o[20] = bloom ? (bloom_check20(bloom, g, h) ? 1 : 0) : 0;
 }
 
 // Field self-test: the fast (fe_asm.hpp) operations, results canonicalised.
@@ -439,7 +537,12 @@ struct khb_ctx {
   AffPt* h_centres = nullptr;          // pinned staging
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool in_flight = false;
+  bool addr_in_flight = false;
   uint64_t pending_steps = 0;
+  // -m address
+  uint8_t* d_abloom = nullptr;
+  BloomGeom ageom{};
+  uint32_t* d_ahits = nullptr;
 };
 
 namespace {
@@ -494,12 +597,14 @@ ScanArgs make_args(khb_ctx* c, uint32_t n_jobs, uint32_t group_begin, uint32_t g
   return A;
 }
 
-int check_scan_args(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count) {
+int check_scan_args(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count,
+                    bool bsgs = true) {
   if (!c || !centres || n_jobs == 0 || group_count == 0) return KHB_EINVAL;
   if (!c->d_gsn || !c->d_offs || c->gpl == 0) return KHB_ESTATE;
   if (group_begin % c->gpl) return KHB_EINVAL;
   uint64_t end = (uint64_t)group_begin + group_count;
-  if (end * KHB_GROUP > 0xFFFFFFFFull) return KHB_EINVAL;         // a = j*1024+t fits 32 bits (keyhunt.cpp:3948)
+  if (end > 0xFFFFFFFFull) return KHB_EINVAL;
+  if (bsgs && end * KHB_GROUP > 0xFFFFFFFFull) return KHB_EINVAL;  // a = j*1024+t fits 32 bits (keyhunt.cpp:3948)
   if ((end + c->gpl - 1) / c->gpl > c->n_offs) return KHB_EINVAL;  // offsets table too short
   return KHB_OK;
 }
@@ -575,6 +680,8 @@ int khb_close(khb_ctx* c) {
   hipFree(c->d_cand);
   hipFree(c->d_degen);
   hipFree(c->d_counters);
+  hipFree(c->d_abloom);
+  hipFree(c->d_ahits);
   if (c->h_counters) hipHostFree(c->h_counters);
   if (c->h_centres) hipHostFree(c->h_centres);
   if (c->ev0) hipEventDestroy(c->ev0);
@@ -633,7 +740,7 @@ int khb_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t gro
   int rc = check_scan_args(c, centres, n_jobs, group_begin, group_count);
   if (rc) return rc;
   if (!c->d_bloom) return KHB_ESTATE;
-  if (c->in_flight) return KHB_EBUSY;
+  if (c->in_flight || c->addr_in_flight) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
   if ((rc = ensure_centres(c, n_jobs))) return rc;
   pts_from_be(c->h_centres, centres, n_jobs);
@@ -642,7 +749,7 @@ int khb_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t gro
   ScanArgs A = make_args(c, n_jobs, group_begin, group_count);
   const uint32_t blocks = c->lanes / kBlock;
   KHB_TRY(c, hipEventRecord(c->ev0, c->stream));
-  hipLaunchKernelGGL(k_giant_scan<false>, dim3(blocks), dim3(kBlock), 0, c->stream, A);
+  hipLaunchKernelGGL(k_giant_scan<kScan>, dim3(blocks), dim3(kBlock), 0, c->stream, A);
   KHB_TRY(c, hipGetLastError());
   KHB_TRY(c, hipEventRecord(c->ev1, c->stream));
   KHB_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, 16, hipMemcpyDeviceToHost, c->stream));
@@ -699,7 +806,7 @@ int khb_dump_x(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint32_t
     ScanArgs A = make_args(c, 1, group_begin, group_count);
     A.xdump = d_x;
     const uint32_t blocks = (uint32_t)((A.n_items + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_giant_scan<true>, dim3(blocks < c->lanes / kBlock ? blocks : c->lanes / kBlock),
+    hipLaunchKernelGGL(k_giant_scan<kDump>, dim3(blocks < c->lanes / kBlock ? blocks : c->lanes / kBlock),
                        dim3(kBlock), 0, c->stream, A);
     e = hipGetLastError();
   }
@@ -756,6 +863,138 @@ int khb_probe(khb_ctx* c, const uint8_t* xs, uint8_t* hit, uint32_t n) {
   if (e == hipSuccess) e = hipMemcpy(hit, dh, n, hipMemcpyDeviceToHost);
   hipFree(d);
   hipFree(dh);
+  free(h);
+  if (e != hipSuccess) return hip_fail(c, e);
+  return KHB_OK;
+}
+
+
+// ---------------------------------------------------------------------------------- -m address
+int khb_load_addr_bloom(khb_ctx* c, const uint8_t* bf, uint64_t bytes, uint64_t bits, uint32_t hashes) {
+  if (!c || !bf || bytes == 0 || bits < 2 || hashes == 0 || hashes > 255) return KHB_EINVAL;
+  if ((bits + 7) / 8 != bytes) return KHB_EINVAL;    // bloom.cpp:110-113
+  if (c->in_flight || c->addr_in_flight) return KHB_EBUSY;
+  KHB_TRY(c, hipSetDevice(c->device));
+  if (c->d_abloom) { hipFree(c->d_abloom); c->d_abloom = nullptr; }
+  KHB_TRY(c, hipMalloc(&c->d_abloom, bytes));
+  KHB_TRY(c, hipMemcpy(c->d_abloom, bf, bytes, hipMemcpyHostToDevice));
+  c->ageom.bytes_per_sub = bytes;
+  c->ageom.bits = bits;
+  c->ageom.magic = (uint64_t)(((unsigned __int128)1 << 64) / bits);
+  c->ageom.wrap = (uint64_t)(((unsigned __int128)1 << 64) % bits);
+  c->ageom.hashes = hashes;
+  if (!c->d_ahits) KHB_TRY(c, hipMalloc(&c->d_ahits, sizeof(khb_addr_hit) * kAddrHitCap));
+  return KHB_OK;
+}
+
+int khb_addr_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count,
+                    int search) {
+  int rc = check_scan_args(c, centres, n_jobs, group_begin, group_count, false);
+  if (rc) return rc;
+  if (search < 0 || search > 2) return KHB_EINVAL;
+  if (!c->d_abloom) return KHB_ESTATE;
+  if (c->in_flight || c->addr_in_flight) return KHB_EBUSY;
+  KHB_TRY(c, hipSetDevice(c->device));
+  if ((rc = ensure_centres(c, n_jobs))) return rc;
+  pts_from_be(c->h_centres, centres, n_jobs);
+  KHB_TRY(c, hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, c->stream));
+  KHB_TRY(c, hipMemsetAsync(c->d_counters, 0, 16, c->stream));
+  ScanArgs A = make_args(c, n_jobs, group_begin, group_count);
+  A.bloom = c->d_abloom;
+  A.geom = c->ageom;
+  A.ahits = c->d_ahits;
+  A.ahit_cap = kAddrHitCap;
+  const uint32_t blocks = c->lanes / kBlock;
+  KHB_TRY(c, hipEventRecord(c->ev0, c->stream));
+  switch (search) {
+    case 0: hipLaunchKernelGGL(k_giant_scan<kAddrU>, dim3(blocks), dim3(kBlock), 0, c->stream, A); break;
+    case 1: hipLaunchKernelGGL(k_giant_scan<kAddrC>, dim3(blocks), dim3(kBlock), 0, c->stream, A); break;
+    default: hipLaunchKernelGGL(k_giant_scan<kAddrB>, dim3(blocks), dim3(kBlock), 0, c->stream, A); break;
+  }
+  KHB_TRY(c, hipGetLastError());
+  KHB_TRY(c, hipEventRecord(c->ev1, c->stream));
+  KHB_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, 16, hipMemcpyDeviceToHost, c->stream));
+  c->addr_in_flight = true;
+  c->pending_steps = (uint64_t)n_jobs * group_count * KHB_GROUP;
+  return KHB_OK;
+}
+
+int khb_addr_collect(khb_ctx* c, khb_addr_hit* hits, uint32_t cap, khb_stats* st) {
+  if (!c) return KHB_EINVAL;
+  if (!c->addr_in_flight) return KHB_ESTATE;
+  KHB_TRY(c, hipSetDevice(c->device));
+  c->addr_in_flight = false;
+  KHB_TRY(c, hipStreamSynchronize(c->stream));
+  const uint32_t nh = c->h_counters[0], nd = c->h_counters[1];
+  uint32_t take = nh < kAddrHitCap ? nh : kAddrHitCap;
+  if (take > cap) take = cap;
+  if (take && hits) KHB_TRY(c, hipMemcpy(hits, c->d_ahits, sizeof(khb_addr_hit) * take, hipMemcpyDeviceToHost));
+  if (st) {
+    st->n_cand = nh;
+    st->n_degenerate = nd;
+    st->giant_steps = c->pending_steps;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) ms = -1.f;
+    st->kernel_ms = ms;
+  }
+  return KHB_OK;
+}
+
+int khb_addr_scan(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count,
+                  int search, khb_addr_hit* hits, uint32_t cap, khb_stats* st) {
+  int rc = khb_addr_submit(c, centres, n_jobs, group_begin, group_count, search);
+  if (rc) return rc;
+  return khb_addr_collect(c, hits, cap, st);
+}
+
+int khb_addr_dump(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint32_t group_count, uint8_t* xy) {
+  int rc = check_scan_args(c, centre, 1, group_begin, group_count, false);
+  if (rc) return rc;
+  if (!xy) return KHB_EINVAL;
+  if (c->in_flight || c->addr_in_flight) return KHB_EBUSY;
+  KHB_TRY(c, hipSetDevice(c->device));
+  if ((rc = ensure_centres(c, 1))) return rc;
+  pts_from_be(c->h_centres, centre, 1);
+  const size_t bytes = (size_t)group_count * KHB_GROUP * 64;
+  uint8_t* d_xy = nullptr;
+  KHB_TRY(c, hipMalloc(&d_xy, bytes));
+  hipError_t e = hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, 16, c->stream);
+  if (e == hipSuccess) {
+    ScanArgs A = make_args(c, 1, group_begin, group_count);
+    A.xdump = d_xy;
+    const uint32_t blocks = (uint32_t)((A.n_items + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_giant_scan<kAddrDump>, dim3(blocks < c->lanes / kBlock ? blocks : c->lanes / kBlock),
+                       dim3(kBlock), 0, c->stream, A);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipMemcpy(xy, d_xy, bytes, hipMemcpyDeviceToHost);
+  hipFree(d_xy);
+  if (e != hipSuccess) return hip_fail(c, e);
+  return KHB_OK;
+}
+
+int khb_hash160(khb_ctx* c, int kind, const uint8_t* xy, uint8_t* out, uint32_t n) {
+  if (!c || !xy || !out || n == 0 || kind < 0 || kind > 2) return KHB_EINVAL;
+  KHB_TRY(c, hipSetDevice(c->device));
+  AffPt* h = (AffPt*)malloc(sizeof(AffPt) * n);
+  if (!h) return KHB_ENOMEM;
+  pts_from_be(h, xy, n);
+  AffPt* d = nullptr;
+  uint8_t* dout = nullptr;
+  hipError_t e = hipMalloc(&d, sizeof(AffPt) * n);
+  if (e == hipSuccess) e = hipMalloc(&dout, 21 * (size_t)n);
+  if (e == hipSuccess) e = hipMemcpy(d, h, sizeof(AffPt) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_hash160, dim3((n + 255) / 256), dim3(256), 0, c->stream, (const Fe*)d, kind, c->d_abloom,
+                       c->ageom, dout, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipMemcpy(out, dout, 21 * (size_t)n, hipMemcpyDeviceToHost);
+  hipFree(d);
+  hipFree(dout);
   free(h);
   if (e != hipSuccess) return hip_fail(c, e);
   return KHB_OK;

@@ -27,6 +27,10 @@ class Degenerate(C.Structure):
     _fields_ = [("job", C.c_uint32), ("group", C.c_uint32)]
 
 
+class AddrHit(C.Structure):
+    _fields_ = [("job", C.c_uint32), ("group", C.c_uint32), ("t", C.c_uint32), ("kind", C.c_uint32)]
+
+
 class Stats(C.Structure):
     _fields_ = [("n_cand", C.c_uint32), ("n_degenerate", C.c_uint32), ("giant_steps", C.c_uint64),
                 ("kernel_ms", C.c_float)]
@@ -63,6 +67,13 @@ def lib(path: str | None = None) -> C.CDLL:
         L.khb_dump_x.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_char_p]
         L.khb_field_op.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint32]
         L.khb_probe.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_uint32]
+        L.khb_load_addr_bloom.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, C.c_uint64, C.c_uint32]
+        L.khb_addr_submit.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int]
+        L.khb_addr_collect.argtypes = [C.c_void_p, P(AddrHit), C.c_uint32, P(Stats)]
+        L.khb_addr_scan.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
+                                    P(AddrHit), C.c_uint32, P(Stats)]
+        L.khb_addr_dump.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_char_p]
+        L.khb_hash160.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_char_p, C.c_uint32]
         _libs[path] = L
     return _libs[path]
 
@@ -153,3 +164,29 @@ class Engine:
         out = C.create_string_buffer(n)
         _check(self.L.khb_probe(self.h, xs, out, n), self.h, self.L)
         return out.raw
+
+    # ---- -m address ----
+    def load_addr_bloom(self, bf: bytes, bits: int, hashes: int) -> None:
+        _check(self.L.khb_load_addr_bloom(self.h, bf, len(bf), bits, hashes), self.h, self.L)
+
+    def addr_scan(self, centres: bytes, group_begin: int, group_count: int, search: int = 2, cap: int = 1 << 18):
+        """Bloom hits [(job, group, t, kind)] of -m address over group_count groups of each job."""
+        hits = (AddrHit * cap)()
+        st = Stats()
+        _check(self.L.khb_addr_scan(self.h, centres, len(centres) // 64, group_begin, group_count, search, hits, cap,
+                                    C.byref(st)), self.h, self.L)
+        n = min(st.n_cand, cap)
+        return [(int(hits[i].job), int(hits[i].group), int(hits[i].t), int(hits[i].kind)) for i in range(n)], st
+
+    def addr_dump(self, centre: bytes, group_begin: int, group_count: int) -> bytes:
+        out = C.create_string_buffer(group_count * KHB_GROUP * 64)
+        _check(self.L.khb_addr_dump(self.h, centre, group_begin, group_count, out), self.h, self.L)
+        return out.raw
+
+    def hash160(self, kind: int, xy: bytes) -> list[tuple[bytes, int]]:
+        """[(hash160, bloom bit)] of each x||y point for kind 0/1 (compressed 02/03) or 2."""
+        n = len(xy) // 64
+        out = C.create_string_buffer(21 * n)
+        _check(self.L.khb_hash160(self.h, kind, xy, out, n), self.h, self.L)
+        r = out.raw
+        return [(r[21 * i:21 * i + 20], r[21 * i + 20]) for i in range(n)]

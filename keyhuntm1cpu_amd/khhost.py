@@ -48,6 +48,22 @@ def lib() -> C.CDLL:
         L.khh_session_close.argtypes = [C.c_void_p]
         L.khh_pubkey.argtypes = [C.c_char_p, C.c_char_p]
         L.khh_parse_pubkey.argtypes = [C.c_char_p, C.c_char_p, P(C.c_int)]
+        L.khh_addr_new.restype = C.c_void_p
+        L.khh_addr_new.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_uint64, C.c_uint32, C.c_int, C.c_char_p,
+                                   C.c_size_t]
+        L.khh_addr_free.argtypes = [C.c_void_p]
+        L.khh_addr_table.restype = P(C.c_uint8)
+        L.khh_addr_table.argtypes = [C.c_void_p, P(C.c_uint64)]
+        L.khh_addr_bloom.restype = P(C.c_uint8)
+        L.khh_addr_bloom.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_uint32)]
+        L.khh_addr_giant_table.argtypes = [C.c_void_p, C.c_char_p]
+        L.khh_addr_lane_offsets.restype = C.c_uint32
+        L.khh_addr_lane_offsets.argtypes = [C.c_void_p, C.c_char_p, P(C.c_uint32)]
+        L.khh_addr_search.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int, C.c_int, P(C.c_int), C.c_int,
+                                      C.c_uint32, C.c_uint64, C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint32,
+                                      P(C.c_uint32), P(C.c_uint64), C.c_char_p, C.c_size_t]
+        L.khh_hash160.argtypes = [C.c_char_p, C.c_int, C.c_char_p]
+        L.khh_rmd_to_address.argtypes = [C.c_char_p, C.c_char_p]
         _lib = L
     return _lib
 
@@ -196,3 +212,88 @@ class Session:
         st = {k: int(stats[i]) for i, k in enumerate(_STAT_KEYS)}
         st["kernel_s"] = stats[4] / 1e6
         return res, st
+
+
+# ---- -m address / -m rmd160 ----
+def hash160(xy: bytes, compressed: bool) -> bytes:
+    out = C.create_string_buffer(20)
+    lib().khh_hash160(xy, 1 if compressed else 0, out)
+    return out.raw
+
+
+def rmd_to_address(rmd: bytes) -> str:
+    out = C.create_string_buffer(64)
+    lib().khh_rmd_to_address(rmd, out)
+    return out.value.decode()
+
+
+class Addr:
+    """-m address targets (a target file's text) + generator for chunks of n_seq keys."""
+
+    def __init__(self, text: str, n_seq: int = 1 << 32, stride: int = 1, gpl: int = 16, bloom_multiplier: int = 1,
+                 threads: int = 0):
+        err = C.create_string_buffer(256)
+        self.h = lib().khh_addr_new(text.encode(), bloom_multiplier, _b32(stride), n_seq, gpl, threads, err, 256)
+        if not self.h:
+            raise KhhError(err.value.decode())
+        self.n_seq, self.stride = n_seq, stride
+
+    def close(self) -> None:
+        if self.h:
+            lib().khh_addr_free(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def table(self) -> list[bytes]:
+        n = C.c_uint64(0)
+        p = lib().khh_addr_table(self.h, C.byref(n))
+        raw = C.string_at(p, 20 * n.value) if n.value else b""
+        return [raw[20 * i:20 * i + 20] for i in range(n.value)]
+
+    def bloom(self) -> tuple[bytes, int, int]:
+        nb, bits, h = C.c_uint64(0), C.c_uint64(0), C.c_uint32(0)
+        p = lib().khh_addr_bloom(self.h, C.byref(nb), C.byref(bits), C.byref(h))
+        return C.string_at(p, nb.value), int(bits.value), int(h.value)
+
+    def giant_table(self) -> bytes:
+        out = C.create_string_buffer(513 * 64)
+        lib().khh_addr_giant_table(self.h, out)
+        return out.raw
+
+    def lane_offsets(self) -> tuple[bytes, int]:
+        g = C.c_uint32(0)
+        n = lib().khh_addr_lane_offsets(self.h, None, C.byref(g))
+        out = C.create_string_buffer(64 * n)
+        lib().khh_addr_lane_offsets(self.h, out, C.byref(g))
+        return out.raw, int(g.value)
+
+    def search(self, start: int, end: int, search: int = 2, devices=(0,), lanes: int = 0, max_chunks: int = 0,
+               random_chunks: bool = False, cap: int = 4096):
+        """Found [(key, compressed, rmd160)] in discovery order, plus stats."""
+        keys = C.create_string_buffer(32 * cap)
+        comp = C.create_string_buffer(cap)
+        rmd = C.create_string_buffer(20 * cap)
+        nf = C.c_uint32(0)
+        st = (C.c_uint64 * 6)()
+        devs = (C.c_int * len(devices))(*devices)
+        err = C.create_string_buffer(256)
+        rc = lib().khh_addr_search(self.h, _b32(start), _b32(end), search, 1 if random_chunks else 0, devs,
+                                   len(devices), lanes, max_chunks, keys, comp, rmd, cap, C.byref(nf), st, err, 256)
+        if rc:
+            raise KhhError(f"khh_addr_search: {err.value.decode()} [{rc}]")
+        n = min(nf.value, cap)
+        found = [(int.from_bytes(keys.raw[32 * i:32 * i + 32], "big"), bool(comp.raw[i]), rmd.raw[20 * i:20 * i + 20])
+                 for i in range(n)]
+        return found, {"chunks": st[0], "keys": st[1], "hits": st[2], "degenerate": st[3], "kernel_s": st[4] / 1e6,
+                       "launches": st[5]}

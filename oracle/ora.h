@@ -116,6 +116,34 @@ uint64_t ora_bsgs_search(const ora_bsgs* c, const ora_point* targets, int ntarge
 uint64_t ora_bsgs_bench(const ora_bsgs* c, const ora_point* target, const ora_u256* base, int nthreads,
                         double seconds, double* elapsed);
 
+/* ---- -m address / -m rmd160 (ora_addr.c) ---- */
+void ora_sha256(const uint8_t* msg, size_t len, uint8_t out[32]);
+void ora_ripemd160(const uint8_t* msg, size_t len, uint8_t out[20]);
+void ora_hash160(const uint8_t* msg, size_t len, uint8_t out[20]);
+void ora_pub_hash160(const ora_point* p, int compressed, uint8_t out[20]);   /* SECP256K1.cpp:671-705 */
+void ora_x_hash160(uint8_t prefix, const ora_u256* x, uint8_t out[20]);     /* SECP256K1.cpp:707-789 */
+int  ora_b58decode(const char* s, uint8_t* bin, size_t binsz, size_t* outsz); /* base58.c:39-112 */
+void ora_rmd_to_address(const uint8_t rmd[20], char* out);                  /* keyhunt.cpp:2274-2284 */
+
+typedef struct ora_addr ora_addr;
+typedef struct ora_addr_gen ora_addr_gen;
+/* forceReadFileAddress (keyhunt.cpp:6300-6358) over a target file's text; bloom per
+ * initBloomFilter (keyhunt.cpp:6559-6576); table sorted (_sort). */
+ora_addr* ora_addr_new(const char* text, int bloom_multiplier);
+void      ora_addr_free(ora_addr* A);
+uint64_t  ora_addr_count(const ora_addr* A);
+const uint8_t* ora_addr_table(const ora_addr* A);
+const ora_bloom* ora_addr_bloom(const ora_addr* A);
+int       ora_addr_searchbinary(const ora_addr* A, const uint8_t data[20]);   /* keyhunt.cpp:2311-2335 */
+/* init_generator (keyhunt.cpp:4386-4399): Gn[i] = (i+1)*stride*G, _2Gn = 1024*stride*G */
+ora_addr_gen* ora_addr_gen_new(const ora_u256* stride);
+void      ora_addr_gen_free(ora_addr_gen* g);
+void      ora_addr_gen_table(const ora_addr_gen* g, uint8_t out[513 * 64]);
+/* one thread_process group (keyhunt.cpp:2586-2711, checks 2789-2937); see ora_addr.c */
+void ora_addr_group(const ora_addr* A, const ora_addr_gen* g, const ora_u256* key, int search, uint8_t* xy,
+                    uint32_t* hits, uint32_t hcap, uint32_t* nhits, ora_u256* keys, uint32_t kcap,
+                    uint32_t* nkeys);
+
 /* ---- flat C-ABI helpers for ctypes (hex/byte strings only) ---- */
 int ora_h_pubkey(const char* khex, char* out_hex, int compressed);       /* pubkey of key */
 int ora_h_parse_target(const char* line, uint8_t xy_be[64], int* compressed);

@@ -105,6 +105,31 @@ def lib() -> C.CDLL:
         L.ora_bloom_add.argtypes = [P(Bloom), C.c_void_p, C.c_int]
         L.ora_bloom_check.restype = C.c_int
         L.ora_bloom_check.argtypes = [P(Bloom), C.c_void_p, C.c_int]
+        L.ora_sha256.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p]
+        L.ora_ripemd160.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p]
+        L.ora_hash160.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p]
+        L.ora_pub_hash160.argtypes = [P(Point), C.c_int, C.c_char_p]
+        L.ora_x_hash160.argtypes = [C.c_uint8, P(U256), C.c_char_p]
+        L.ora_b58decode.restype = C.c_int
+        L.ora_b58decode.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t, P(C.c_size_t)]
+        L.ora_rmd_to_address.argtypes = [C.c_char_p, C.c_char_p]
+        L.ora_addr_new.restype = C.c_void_p
+        L.ora_addr_new.argtypes = [C.c_char_p, C.c_int]
+        L.ora_addr_free.argtypes = [C.c_void_p]
+        L.ora_addr_count.restype = C.c_uint64
+        L.ora_addr_count.argtypes = [C.c_void_p]
+        L.ora_addr_table.restype = C.c_void_p
+        L.ora_addr_table.argtypes = [C.c_void_p]
+        L.ora_addr_bloom.restype = P(Bloom)
+        L.ora_addr_bloom.argtypes = [C.c_void_p]
+        L.ora_addr_searchbinary.restype = C.c_int
+        L.ora_addr_searchbinary.argtypes = [C.c_void_p, C.c_char_p]
+        L.ora_addr_gen_new.restype = C.c_void_p
+        L.ora_addr_gen_new.argtypes = [P(U256)]
+        L.ora_addr_gen_free.argtypes = [C.c_void_p]
+        L.ora_addr_gen_table.argtypes = [C.c_void_p, C.c_char_p]
+        L.ora_addr_group.argtypes = [C.c_void_p, C.c_void_p, P(U256), C.c_int, C.c_void_p, P(C.c_uint32),
+                                     C.c_uint32, P(C.c_uint32), P(U256), C.c_uint32, P(C.c_uint32)]
         _lib = L
     return _lib
 
@@ -232,3 +257,116 @@ class Bsgs:
 # secp256k1 constants (SECP256K1.cpp:31-40)
 P = 2**256 - 2**32 - 977
 ORDER = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+
+
+# ---- -m address / -m rmd160 (ora_addr.c) ----
+def sha256(data: bytes) -> bytes:
+    out = C.create_string_buffer(32)
+    lib().ora_sha256(data, len(data), out)
+    return out.raw
+
+
+def ripemd160(data: bytes) -> bytes:
+    out = C.create_string_buffer(20)
+    lib().ora_ripemd160(data, len(data), out)
+    return out.raw
+
+
+def hash160(data: bytes) -> bytes:
+    out = C.create_string_buffer(20)
+    lib().ora_hash160(data, len(data), out)
+    return out.raw
+
+
+def pub_hash160(p: Point, compressed: bool) -> bytes:
+    out = C.create_string_buffer(20)
+    lib().ora_pub_hash160(C.byref(p), 1 if compressed else 0, out)
+    return out.raw
+
+
+def x_hash160(prefix: int, x: int) -> bytes:
+    out = C.create_string_buffer(20)
+    lib().ora_x_hash160(prefix, C.byref(U256.of(x)), out)
+    return out.raw
+
+
+def b58decode(s: str, size: int = 25) -> tuple[bytes, int] | None:
+    buf = C.create_string_buffer(size)
+    sz = C.c_size_t(0)
+    if not lib().ora_b58decode(s.encode(), buf, size, C.byref(sz)):
+        return None
+    return buf.raw, int(sz.value)
+
+
+def rmd_to_address(rmd: bytes) -> str:
+    out = C.create_string_buffer(64)
+    lib().ora_rmd_to_address(rmd, out)
+    return out.value.decode()
+
+
+class AddrTable:
+    """forceReadFileAddress + initBloomFilter + _sort over a target file's text."""
+
+    def __init__(self, text: str, bloom_multiplier: int = 1):
+        self.h = lib().ora_addr_new(text.encode(), bloom_multiplier)
+
+    def close(self) -> None:
+        if self.h:
+            lib().ora_addr_free(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def n(self) -> int:
+        return int(lib().ora_addr_count(self.h))
+
+    def table(self) -> bytes:
+        return C.string_at(lib().ora_addr_table(self.h), 20 * self.n)
+
+    def bloom(self) -> Bloom:
+        return lib().ora_addr_bloom(self.h).contents
+
+    def bloom_bytes(self) -> bytes:
+        b = self.bloom()
+        return C.string_at(b.bf, b.bytes)
+
+    def bloom_check(self, h20: bytes) -> bool:
+        return bool(lib().ora_bloom_check(lib().ora_addr_bloom(self.h), h20, 20))
+
+    def searchbinary(self, h20: bytes) -> bool:
+        return bool(lib().ora_addr_searchbinary(self.h, h20))
+
+
+class AddrGen:
+    """init_generator: Gn[i] = (i+1)*stride*G, _2Gn = 1024*stride*G."""
+
+    def __init__(self, stride: int = 1):
+        self.h = lib().ora_addr_gen_new(C.byref(U256.of(stride)))
+        self.stride = stride
+
+    def close(self) -> None:
+        if self.h:
+            lib().ora_addr_gen_free(self.h)
+            self.h = None
+
+    def table(self) -> bytes:
+        out = C.create_string_buffer(513 * 64)
+        lib().ora_addr_gen_table(self.h, out)
+        return out.raw
+
+    def group(self, A: AddrTable, key: int, search: int = 2, want_xy: bool = False, cap: int = 1 << 12):
+        """One thread_process group at first key `key`: (hits [(t, kind)], keys, xy bytes|None)."""
+        xy = C.create_string_buffer(1024 * 64) if want_xy else None
+        hits = (C.c_uint32 * cap)()
+        keys = (U256 * cap)()
+        nh, nk = C.c_uint32(0), C.c_uint32(0)
+        lib().ora_addr_group(A.h, self.h, C.byref(U256.of(key)), search, xy, hits, cap, C.byref(nh), keys, cap,
+                             C.byref(nk))
+        hl = [(int(hits[i]) >> 2, int(hits[i]) & 3) for i in range(min(nh.value, cap))]
+        kl = [keys[i].value() for i in range(min(nk.value, cap))]
+        return hl, kl, (xy.raw if want_xy else None)

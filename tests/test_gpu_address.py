@@ -1,0 +1,140 @@
+"""GPU parity for -m address / -m rmd160 (keyhunt.cpp:2586-2937): libkhbsgs through its C ABI and
+the libkhhost search driver, against the oracle restatement.  Bit-exact: every hash160, every
+group point (x||y), every bloom hit (t, kind), every recovered key."""
+from __future__ import annotations
+
+import json
+import os
+import random
+
+import pytest
+
+from keyhuntm1cpu_amd import khhost
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+
+
+def _text(name: str) -> str:
+    with open(os.path.join(GOLD, "address", name)) as f:
+        return f.read()
+
+
+@pytest.fixture(scope="module")
+def keys():
+    with open(os.path.join(GOLD, "puzzle_keys.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from keyhuntm1cpu_amd.khbsgs import Engine
+    e = Engine(0, lanes=16384)
+    yield e
+    e.close()
+
+
+def _load(eng, A: khhost.Addr):
+    bf, bits, h = A.bloom()
+    eng.load_addr_bloom(bf, bits, h)
+    eng.load_giant_table(A.giant_table())
+    offs, gpl = A.lane_offsets()
+    eng.load_lane_offsets(offs, gpl)
+
+
+def test_hash160_kernel_matches_oracle(eng, ora):
+    A = khhost.Addr(_text("1to32.rmd"), n_seq=1 << 16)
+    _load(eng, A)
+    rng = random.Random(11)
+    ks = [1, 2, 3, N - 1] + [rng.randrange(1, N) for _ in range(3000)]
+    pts = [ora.pubkey(k) for k in ks]
+    xy = b"".join(p.be64() for p in pts)
+    O = ora.AddrTable(_text("1to32.rmd"))
+    for kind in (0, 1, 2):
+        got = eng.hash160(kind, xy)
+        for i, p in enumerate(pts):
+            ref = ora.x_hash160(2 + kind, p.x.value()) if kind < 2 else ora.pub_hash160(p, False)
+            assert got[i][0] == ref, (kind, i)
+            assert got[i][1] == (1 if O.bloom_check(ref) else 0)
+    # puzzle keys 1 and 3 are members (compressed, prefix of their own y parity)
+    members = [(ora.pubkey(k), k) for k in (1, 3, 7)]
+    for p, k in members:
+        kind = 1 if p.y.value() & 1 else 0
+        assert eng.hash160(kind, p.be64())[0][1] == 1
+
+
+def _oracle_groups(ora, O, gen, base: int, ngroups: int, search: int):
+    hits, keys = [], []
+    for g in range(ngroups):
+        h, k, _ = gen.group(O, base + 1024 * g, search)
+        hits += [(g, t, kind) for t, kind in h]
+        keys += k
+    return sorted(hits), keys
+
+
+@pytest.mark.parametrize("gpl", [1, 4])
+def test_addr_dump_matches_oracle(eng, ora, gpl):
+    A = khhost.Addr(_text("1to32.rmd"), n_seq=1 << 16, gpl=gpl)
+    _load(eng, A)
+    gen = ora.AddrGen(1)
+    base = 0x123456789ABCDEF0123
+    centre = khhost.pubkey(base + 512)
+    xy = eng.addr_dump(centre, 0, 8)
+    O = ora.AddrTable(_text("1to32.rmd"))
+    for g in range(8):
+        _, _, ref = gen.group(O, base + 1024 * g, 2, want_xy=True)
+        assert xy[g * 65536:(g + 1) * 65536] == ref, g
+
+
+@pytest.mark.parametrize("search", [0, 1, 2])
+def test_addr_hits_match_oracle_dense_targets(eng, ora, search):
+    """A target file holding the hash160s of 3000 keys of the scanned window (compressed for even
+    keys, uncompressed for odd, plus negated keys) makes thousands of true bloom hits; the GPU's hit
+    set must equal the oracle's for every (group, t, kind)."""
+    rng = random.Random(search)
+    base, ngroups = 0x4000000000 + 1, 48
+    picks = rng.sample(range(base, base + 1024 * ngroups), 3000)
+    lines = []
+    for i, k in enumerate(picks):
+        kk = N - k if i % 7 == 0 else k
+        lines.append(ora.pub_hash160(ora.pubkey(kk), i % 2 == 0).hex())
+    text = "\n".join(lines) + "\n"
+    A = khhost.Addr(text, n_seq=1024 * ngroups, gpl=4)
+    _load(eng, A)
+    O = ora.AddrTable(text)
+    gen = ora.AddrGen(1)
+    ref_hits, ref_keys = _oracle_groups(ora, O, gen, base, ngroups, search)
+    hits, st = eng.addr_scan(khhost.pubkey(base + 512), 0, ngroups, search)
+    assert st.giant_steps == 1024 * ngroups
+    assert sorted((g, t, kind) for _, g, t, kind in hits) == ref_hits
+    assert len(ref_hits) > 1000
+    # the host search confirms exactly the oracle's keys
+    found, st2 = A.search(base, base + 1024 * ngroups, search=search, lanes=16384)
+    assert sorted(k for k, _, _ in found) == sorted(ref_keys)
+
+
+def test_addr_search_puzzles(keys):
+    """Puzzles 1..24 from tests/1to32.txt (base58 addresses) in one sequential run of [1, 2^24)."""
+    A = khhost.Addr(_text("1to32.txt"), n_seq=1 << 20)
+    found, st = A.search(1, 1 << 24, search=2, lanes=65536)
+    got = sorted(k for k, c, _ in found)
+    assert got == sorted(int(keys[str(n)]["key"], 16) for n in range(1, 25))
+    assert all(c for _, c, _ in found)
+    assert st["chunks"] == 16 and st["keys"] == 1 << 24
+
+
+def test_addr_search_uncompressed_and_negated():
+    k = 0x5A5A5A123
+    xy_k = khhost.pubkey(k)
+    xy_nk = khhost.pubkey(N - k)
+    text = "\n".join([khhost.hash160(xy_k, False).hex(),                       # uncompressed of k
+                      khhost.rmd_to_address(khhost.hash160(xy_nk, True))]) + "\n"   # compressed of n-k
+    A = khhost.Addr(text, n_seq=1 << 20)
+    lo, hi = k - (k % (1 << 20)), k - (k % (1 << 20)) + (1 << 20)
+    f2, _ = A.search(lo, hi, search=2, lanes=16384)
+    assert sorted((kk, c) for kk, c, _ in f2) == sorted([(k, False), (N - k, True)])
+    f1, _ = A.search(lo, hi, search=1, lanes=16384)
+    assert [(kk, c) for kk, c, _ in f1] == [(N - k, True)]
+    f0, _ = A.search(lo, hi, search=0, lanes=16384)
+    assert [(kk, c) for kk, c, _ in f0] == [(k, False)]
