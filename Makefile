@@ -33,8 +33,9 @@ build/host/%.o: $(CSRC)/host/%.cpp $(HOST_HDRS) | build/host
 $(LIBDIR)/libkhhost.so: $(HOST_OBJS) build/host/khhost_capi.o $(LIBDIR)/libkhbsgs.so
 	$(CXX) $(CXXFLAGS) -shared -o $@ $(HOST_OBJS) build/host/khhost_capi.o -L$(LIBDIR) -lkhbsgs -Wl,-rpath,'$$ORIGIN'
 
-$(BINDIR)/keyhunt_amd: $(HOST_OBJS) build/host/keyhunt_main.o $(LIBDIR)/libkhbsgs.so | $(BINDIR)
-	$(CXX) $(CXXFLAGS) -o $@ $(HOST_OBJS) build/host/keyhunt_main.o -L$(LIBDIR) -lkhbsgs -Wl,-rpath,'$$ORIGIN/../lib'
+CLI_OBJS := build/host/keyhunt_main.o build/host/keyhunt_address.o
+$(BINDIR)/keyhunt_amd: $(HOST_OBJS) $(CLI_OBJS) $(LIBDIR)/libkhbsgs.so | $(BINDIR)
+	$(CXX) $(CXXFLAGS) -o $@ $(HOST_OBJS) $(CLI_OBJS) -L$(LIBDIR) -lkhbsgs -Wl,-rpath,'$$ORIGIN/../lib'
 
 oracle:
 	$(MAKE) -s -C oracle

@@ -23,6 +23,7 @@
 
 #include "../../../include/khbsgs.h"
 #include "bsgs_host.hpp"
+#include "cli.hpp"
 #include "engine.hpp"
 
 using namespace khb;
@@ -106,6 +107,10 @@ U256 rand_range(const U256& lo, const U256& hi) {
   return lo + r;
 }
 
+}  // namespace
+
+namespace khb {
+
 std::string speed_line(const U256& total, uint64_t seconds) {   // keyhunt.cpp:2194-2238
   U256 per = total, q;
   U256::divmod(total, U256(seconds ? seconds : 1), &per, nullptr);
@@ -131,7 +136,7 @@ std::string speed_line(const U256& total, uint64_t seconds) {   // keyhunt.cpp:2
   return buf;
 }
 
-}  // namespace
+}  // namespace khb
 
 int main(int argc, char** argv) {
   setvbuf(stdout, nullptr, _IOLBF, 0);
@@ -146,6 +151,9 @@ int main(int argc, char** argv) {
   int bitrange = 0;
   SearchConfig cfg;
   uint32_t gpu_blocks = 0;
+  AddressCli ao;
+  bool endomorphism = false, eth = false;
+  const char* kSearch[3] = {"uncompress", "compress", "both"};   // keyhunt.cpp:230
   if (nthreads > 16) nthreads = 16;
   static struct option longopts[] = {{"gpu", no_argument, nullptr, 1000},
                                      {"gpu-threads", required_argument, nullptr, 1001},
@@ -175,7 +183,22 @@ int main(int argc, char** argv) {
         }
         break;
       case 'd': printf("[+] Flag DEBUG enabled\n"); break;
-      case 'e': printf("[+] Endomorphism enabled\n"); break;
+      case 'e': endomorphism = true; printf("[+] Endomorphism enabled\n"); break;
+      case 'c': {
+        const char* cryptos[2] = {"btc", "eth"};
+        const int v = index_of(optarg, cryptos, 2);
+        if (v == 1) { eth = true; printf("[+] Setting search for ETH adddress.\n"); }
+        if (v >= 0) ao.crypto_set = true;
+        break;
+      }
+      case 'I': ao.stride = optarg; break;
+      case 'l':
+        switch (index_of(optarg, kSearch, 3)) {
+          case 0: ao.search = 0; printf("[+] Search uncompress only\n"); break;
+          case 1: ao.search = 1; printf("[+] Search compress only\n"); break;
+          case 2: ao.search = 2; printf("[+] Search both compress and uncompress\n"); break;
+        }
+        break;
       case 'f': file = optarg; break;
       case 'k':
         kfactor = (int)strtol(optarg, nullptr, 10);
@@ -186,6 +209,8 @@ int main(int argc, char** argv) {
       case 'm':
         mode = index_of(optarg, kModes, 7);
         if (mode < 0) { fprintf(stderr, "[E] Unknow mode value %s\n", optarg); exit(EXIT_FAILURE); }
+        if (mode == 1) printf("[+] Mode address\n");
+        if (mode == 3) printf("[+] Mode rmd160\n");
         break;
       case 'n': str_n = optarg; break;
       case 'q': quiet = true; printf("[+] Quiet thread output\n"); break;
@@ -230,17 +255,66 @@ int main(int argc, char** argv) {
       case 1001: break;                             // --gpu-threads: fixed 256-lane workgroups
       case 1002: gpu_blocks = (uint32_t)strtoul(optarg, nullptr, 10); break;
       case 1003: cfg.max_chunks = strtoull(optarg, nullptr, 10); break;
-      case 'c': case 'C': case 'E': case 'I': case 'l': case 'N': case 'p': case 'v': case 'G': case '8': case 'z':
+      case 'C': case 'E': case 'N': case 'p': case 'v': case 'G': case '8': case 'z':
         break;   // options of the other search modes
       default:
         fprintf(stderr, "[E] Unknow opcion -%c\n", c);
         exit(EXIT_FAILURE);
     }
   }
+  if (mode == 1 || mode == 3) {
+    if (eth) {
+      fprintf(stderr, "[E] keyhunt_amd searches BTC P2PKH addresses only (-c eth is not available)\n");
+      exit(EXIT_FAILURE);
+    }
+    if (endomorphism) {
+      fprintf(stderr, "[E] keyhunt_amd does not implement -e (endomorphism) for -m %s\n", kModes[mode]);
+      exit(EXIT_FAILURE);
+    }
+    ao.mode = mode;
+    ao.random = bsgs_mode == 3;
+    ao.quiet = quiet;
+    ao.file = file;
+    ao.str_n = str_n;
+    ao.devices = cfg.devices;
+    ao.lanes = gpu_blocks * 256u;
+    ao.max_chunks = cfg.max_chunks;
+    ao.out_seconds = out_seconds;
+    ao.threads = nthreads;
+    ao.flag_bits = flag_bits;
+    ao.bitrange = bitrange;
+    ao.bits_min = bits_min;
+    ao.bits_max = bits_max;
+    if (flag_range) {   // keyhunt.cpp:816-838
+      U256 a, b;
+      U256::from_hex(range_start.c_str(), a);
+      if (a.is_zero()) a = U256(1);
+      U256::from_hex(range_end.c_str(), b);
+      if (a != b) {
+        if (a < secp_order() && b <= secp_order()) {
+          if (a > b) {
+            fprintf(stderr, "[W] Opps, start range can't be great than end range. Swapping them\n");
+            std::swap(a, b);
+          }
+          ao.have_range = true;
+          ao.start = a;
+          ao.end = b;
+        } else {
+          fprintf(stderr, "[E] Start and End range can't be great than N\nFallback to random mode!\n");
+        }
+      } else {
+        fprintf(stderr, "[E] Start and End range can't be the same\nFallback to random mode!\n");
+      }
+    }
+    return run_address_mode(ao);
+  }
   if (mode != 2) {
-    fprintf(stderr, "[E] keyhunt_amd implements -m bsgs only (mode %s is not available)\n", kModes[mode]);
+    fprintf(stderr, "[E] keyhunt_amd implements -m bsgs, -m address and -m rmd160 (mode %s is not available)\n",
+            kModes[mode]);
     exit(EXIT_FAILURE);
   }
+  // keyhunt.cpp:780-789 reject -e / -I only for the BSGS sub-mode "both" (they compare the sub-mode
+  // with MODE_BSGS); that sub-mode is refused below, so -e / -I are ignored here as there.
   if (bsgs_mode != 0 && bsgs_mode != 3) {
     fprintf(stderr, "[E] BSGS mode %s is not implemented by keyhunt_amd yet\n", kBsgsModes[bsgs_mode]);
     exit(EXIT_FAILURE);

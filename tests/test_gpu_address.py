@@ -138,3 +138,36 @@ def test_addr_search_uncompressed_and_negated():
     assert [(kk, c) for kk, c, _ in f1] == [(N - k, True)]
     f0, _ = A.search(lo, hi, search=0, lanes=16384)
     assert [(kk, c) for kk, c, _ in f0] == [(k, False)]
+
+
+def _cli(args, cwd):
+    import subprocess
+    from keyhuntm1cpu_amd import BIN_DIR
+    exe = os.path.join(BIN_DIR, "keyhunt_amd")
+    return subprocess.run([exe] + args, cwd=cwd, capture_output=True, text=True, timeout=300)
+
+
+def test_cli_address_puzzle20(tmp_path, keys):
+    """keyhunt_amd -m address -f tests/1to32.txt -b 20 -n 0x100000: the reference's hit lines and
+    KEYFOUNDKEYFOUND.txt entry for puzzle #20, then End (the range is scanned to its end)."""
+    r = _cli(["-m", "address", "-f", os.path.join(GOLD, "address", "1to32.txt"), "-b", "20", "-n", "0x100000",
+              "-q", "-s", "0"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    k = int(keys["20"]["key"], 16)
+    assert f"Hit! Private Key: {k:x}\n" in r.stdout
+    assert f"pubkey: {keys['20']['pubkey']}\n" in r.stdout
+    assert "Address 1HsMJxNiV7TLxmoF6uJNkydxPFDog4NQum\n" in r.stdout
+    assert r.stdout.rstrip().endswith("End")
+    with open(tmp_path / "KEYFOUNDKEYFOUND.txt") as f:
+        assert f"Private Key: {k:x}" in f.read()
+
+
+def test_cli_rmd160_compress_range(tmp_path, keys):
+    """-m rmd160 with the hash160 file, -l compress, -r window around puzzle #25."""
+    k = int(keys["25"]["key"], 16)
+    lo = k - (k % (1 << 20))
+    r = _cli(["-m", "rmd160", "-f", os.path.join(GOLD, "address", "1to32.rmd"), "-r", f"{lo:x}:{lo + (1 << 21):x}",
+              "-n", "0x100000", "-l", "compress", "-q", "-s", "0"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert f"Hit! Private Key: {k:x}\n" in r.stdout
+    assert "[+] Search compress only" in r.stdout
