@@ -15,7 +15,8 @@ CXXFLAGS ?= -O3 -std=c++17 -fPIC -march=x86-64-v3 -Wall -Wextra -Wno-unused-func
 
 DEV_HDRS  := $(wildcard $(CSRC)/device/*.hpp) include/khbsgs.h
 HOST_SRCS := $(CSRC)/host/u256.cpp $(CSRC)/host/secp_host.cpp $(CSRC)/host/bloom_host.cpp \
-             $(CSRC)/host/bsgs_host.cpp $(CSRC)/host/engine.cpp $(CSRC)/host/address_host.cpp
+             $(CSRC)/host/bsgs_host.cpp $(CSRC)/host/bsgs_files.cpp $(CSRC)/host/engine.cpp \
+             $(CSRC)/host/address_host.cpp
 HOST_HDRS := $(wildcard $(CSRC)/host/*.hpp) $(DEV_HDRS) include/khhost.h
 HOST_OBJS := $(patsubst $(CSRC)/host/%.cpp,build/host/%.o,$(HOST_SRCS))
 

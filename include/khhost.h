@@ -23,6 +23,14 @@ typedef struct khh_tables khh_tables;
  * threads: builder threads; gpl: GPU groups per lane (lane-offset table).  NULL on error (err). */
 khh_tables* khh_tables_new(const char* n_str, int k, int threads, uint32_t gpl, char* err, size_t errlen);
 void khh_tables_free(khh_tables* t);
+/* Like khh_tables_new, with -S semantics (keyhunt.cpp:1373-1613, 1881-2025): the reference's table
+ * files keyhunt_bsgs_{4,6,2,7}_*.{blm,tbl} are read from dir when present (checksums verified
+ * unless skip_checksum), only the missing tables are computed, and with save != 0 the missing ones
+ * are written back.  *have receives the mask of files read (1 L1, 2 L2, 4 bPtable, 8 L3). */
+khh_tables* khh_tables_new_files(const char* n_str, int k, int threads, uint32_t gpl, const char* dir,
+                                 int skip_checksum, int save, uint32_t* have, char* err, size_t errlen);
+/* Write all four table files into dir. */
+int khh_tables_save(const khh_tables* t, const char* dir, char* err, size_t errlen);
 /* out: [0]=m [1]=m2 [2]=m3 [3]=aux [4]=cycles [5]=N(low64) [6]=l1 extent [7..9]=bloom entries L1..L3 */
 void khh_params(const khh_tables* t, uint64_t out[10]);
 /* level 1..3, sub-bloom idx 0..255: pointer to the bit array; geometry through the out params */

@@ -120,19 +120,30 @@ bool make_geometry(const char* n_str, int kfactor, Geometry& g, std::string& err
   return true;
 }
 
-bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, std::string& err,
-                   const std::function<void(uint64_t, uint64_t)>& progress) {
+void Tables::prepare(const Geometry& g) {
   geo = g;
   l1.assign(256, BloomFilter());
   l2.assign(256, BloomFilter());
   l3.assign(256, BloomFilter());
+  bp.assign(g.m3, XValue());
+}
+
+bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, std::string& err,
+                   const std::function<void(uint64_t, uint64_t)>& progress, uint32_t have) {
+  if (!have) prepare(g);
+  geo = g;
   for (int i = 0; i < 256; ++i) {
-    if (l1[i].init2(g.items1, kBloomErr) || l2[i].init2(g.items2, kBloomErr) || l3[i].init2(g.items3, kBloomErr)) {
+    if ((!(have & kFileL1) && l1[i].init2(g.items1, kBloomErr)) || (!(have & kFileL2) && l2[i].init2(g.items2, kBloomErr)) ||
+        (!(have & kFileL3) && l3[i].init2(g.items3, kBloomErr))) {
       err = "[E] error bloom_init";
       return false;
     }
   }
-  bp.assign(g.m3, XValue());
+  if (!(have & kFileBp)) bp.assign(g.m3, XValue());
+  const bool need_l1 = !(have & kFileL1), need_l2 = !(have & kFileL2), need_l3 = !(have & kFileL3),
+             need_bp = !(have & kFileBp);
+  // baby steps to walk: all of the L1 extent, or only the first m2 when L1 came from a file
+  const uint64_t extent = need_l1 ? g.l1ext : ((need_l2 || need_l3 || need_bp) ? g.m2 : 0);
   // giant tables (keyhunt.cpp:1309-1364)
   {
     Pt bsP = negation(mul_g(g.M_double));
@@ -168,9 +179,10 @@ bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, st
   // build jobs (keyhunt.cpp:1739-1807): [from, to) of 2^20 keys, last job overshooting (quirk vi)
   struct Job { uint64_t from, to; };
   std::vector<Job> jobs;
-  {
-    uint64_t W = kJobKeys >= g.m ? g.m : kJobKeys;
-    uint64_t cyc = g.m / W, R = g.m % W;
+  if (extent) {
+    const uint64_t span = need_l1 ? g.m : extent;   // with L1 from a file: the m2 rebuild jobs
+    uint64_t W = kJobKeys >= span ? span : kJobKeys;
+    uint64_t cyc = span / W, R = span % W;
     if (R) cyc++;
     uint64_t base = 0;
     for (uint64_t j = 0; j < cyc; ++j) {
@@ -197,12 +209,14 @@ bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, st
           fe_to_be(xb, xs[t]);
           const int idx = xb[0];
           if (ic < g.m3) {
-            memcpy(bp[ic].value, xb + 16, 6);
-            bp[ic].index = ic;
-            l3[idx].add32_atomic(xb);
+            if (need_bp) {
+              memcpy(bp[ic].value, xb + 16, 6);
+              bp[ic].index = ic;
+            }
+            if (need_l3) l3[idx].add32_atomic(xb);
           }
-          if (ic < g.m2) l2[idx].add32_atomic(xb);
-          if (ic < to) l1[idx].add32_atomic(xb);
+          if (need_l2 && ic < g.m2) l2[idx].add32_atomic(xb);
+          if (need_l1 && ic < to) l1[idx].add32_atomic(xb);
         }
         done.fetch_add(kGrp);
       }
@@ -218,17 +232,18 @@ bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, st
   std::vector<std::thread> th;
   for (int t = 0; t < nthreads; ++t) th.emplace_back(worker);
   while (progress && finished.load() < nthreads) {
-    progress(done.load(), g.l1ext);
+    progress(done.load(), extent);
     std::this_thread::sleep_for(std::chrono::milliseconds(250));
   }
   for (auto& x : th) x.join();
-  if (progress) progress(g.l1ext, g.l1ext);
+  if (progress) progress(extent, extent);
   // bsgs_sort (keyhunt.cpp:3657-3746): for distinct 6-byte keys any correct sort gives the same
   // array; equal keys (SURVEY §8a quirk v) are ordered by index here.
-  std::sort(bp.begin(), bp.end(), [](const XValue& a, const XValue& b) {
-    int r = memcmp(a.value, b.value, 6);
-    return r ? r < 0 : a.index < b.index;
-  });
+  if (need_bp)
+    std::sort(bp.begin(), bp.end(), [](const XValue& a, const XValue& b) {
+      int r = memcmp(a.value, b.value, 6);
+      return r ? r < 0 : a.index < b.index;
+    });
   return true;
 }
 

@@ -34,6 +34,11 @@ struct XValue {            // struct bsgs_xvalue, keyhunt.cpp:70-73
   uint64_t index;
 };
 
+// -S table files (keyhunt.cpp:1373-1613 read, 1881-2025 write): which of them a Tables holds
+// from disk.  Bits: 1 = L1 keyhunt_bsgs_4_<m>.blm, 2 = L2 _6_<m2>.blm, 4 = bPtable _2_<m3>.tbl,
+// 8 = L3 _7_<m3>.blm.
+enum : uint32_t { kFileL1 = 1, kFileL2 = 2, kFileBp = 4, kFileL3 = 8, kFileAll = 15 };
+
 struct Tables {
   Geometry geo;
   std::vector<BloomFilter> l1, l2, l3;   // 256 sub-blooms each
@@ -42,9 +47,20 @@ struct Tables {
   uint32_t gpl = 0;                      // GPU groups per lane
   std::vector<Pt> lane_offs;             // offs[m] = (m*gpl) * _2GSn
 
-  // progress(done, total) is called from the builder threads' coordinator.
+  // progress(done, total) is called from the builder threads' coordinator.  `have` marks tables
+  // already loaded from -S files (load_files): their baby-step work is skipped, and with L1 loaded
+  // only the first m2 baby steps are walked (keyhunt.cpp:1617-1700, "only 3% of the work").
   bool build(const Geometry& g, int nthreads, uint32_t groups_per_lane, std::string& err,
-             const std::function<void(uint64_t, uint64_t)>& progress = nullptr);
+             const std::function<void(uint64_t, uint64_t)>& progress = nullptr, uint32_t have = 0);
+  // -S: read the reference's table files for this geometry from dir (prepare() first).  Returns the
+  // kFile* mask read; false + err on a short read or checksum mismatch (the reference exits).
+  void prepare(const Geometry& g);
+  bool load_files(const std::string& dir, bool skip_checksum, uint32_t& have, std::string& err,
+                  const std::function<void(const std::string&)>& log) ;
+  // -S: write every table not in `have` in the reference's format.
+  bool save_files(const std::string& dir, uint32_t have, std::string& err,
+                  const std::function<void(const std::string&)>& log) const;
+  static std::string file_name(const Geometry& g, uint32_t which);
   std::vector<uint8_t> l1_concat() const;
   std::vector<uint8_t> giant_table_be() const;
   std::vector<uint8_t> lane_offsets_be() const;

@@ -152,6 +152,7 @@ int main(int argc, char** argv) {
   SearchConfig cfg;
   uint32_t gpu_blocks = 0;
   AddressCli ao;
+  bool save_read_file = false, skip_checksum = false;
   bool endomorphism = false, eth = false;
   const char* kSearch[3] = {"uncompress", "compress", "both"};   // keyhunt.cpp:230
   if (nthreads > 16) nthreads = 16;
@@ -164,7 +165,7 @@ int main(int argc, char** argv) {
   while ((c = getopt_long(argc, argv, "deh6MqRSB:b:c:C:E:f:I:k:l:m:N:n:p:r:s:t:v:G:8:z:g:", longopts, nullptr)) != -1) {
     switch (c) {
       case 'h': menu(); break;
-      case '6': fprintf(stderr, "[W] Skipping checksums on files\n"); break;
+      case '6': skip_checksum = true; fprintf(stderr, "[W] Skipping checksums on files\n"); break;
       case 'B': {
         int v = index_of(optarg, kBsgsModes, 5);
         if (v >= 0) bsgs_mode = v; else fprintf(stderr, "[W] Ignoring unknow bsgs mode %s\n", optarg);
@@ -233,7 +234,7 @@ int main(int argc, char** argv) {
         if (out_seconds == 0) printf("[+] Turn off stats output\n");
         else printf("[+] Stats output every %llu seconds\n", (unsigned long long)out_seconds);
         break;
-      case 'S': fprintf(stderr, "[W] -S table files are not supported yet; tables are rebuilt\n"); break;
+      case 'S': save_read_file = true; break;
       case 't':
         nthreads = (int)strtol(optarg, nullptr, 10);
         if (nthreads <= 0) nthreads = 1;
@@ -415,17 +416,38 @@ int main(int argc, char** argv) {
     printf("[+] Bloom filter for %llu elements : %.2f MB\n", (unsigned long long)geo.m3, mb(b.bytes * 256));
     printf("[+] Allocating %.2f MB for %llu bP Points\n", (double)(geo.m3 * 16 / 1048576), (unsigned long long)geo.m3);
   }
-  if (!T.build(geo, nthreads, 4, err, [&](uint64_t d, uint64_t tot) {
-        printf("\r[+] processing %llu/%llu bP points : %i%%\r", (unsigned long long)d, (unsigned long long)tot,
-               (int)((double)d / (double)tot * 100));
-        fflush(stdout);
-      })) {
+  // -S: the reference's table files in the working directory (keyhunt.cpp:1373-1613)
+  uint32_t have = 0;
+  auto say = [](const std::string& m) { printf("%s", m.c_str()); fflush(stdout); };
+  if (save_read_file) {
+    T.prepare(geo);
+    if (!T.load_files(".", skip_checksum, have, err, say)) {
+      fprintf(stderr, "%s\n", err.c_str());
+      exit(EXIT_FAILURE);
+    }
+    if (have && have != kFileAll && (have & kFileL1))
+      printf("[I] We need to recalculate some files, don't worry this is only 3%% of the previous work\n");
+  }
+  if (have != kFileAll || !save_read_file) {
+    if (!T.build(geo, nthreads, 4, err, [&](uint64_t d, uint64_t tot) {
+          printf("\r[+] processing %llu/%llu bP points : %i%%\r", (unsigned long long)d, (unsigned long long)tot,
+                 (int)((double)d / (double)tot * 100));
+          fflush(stdout);
+        }, have)) {
+      fprintf(stderr, "%s\n", err.c_str());
+      exit(EXIT_FAILURE);
+    }
+    const uint64_t ext = (have & kFileL1) ? geo.m2 : geo.l1ext;
+    printf("\r[+] processing %llu/%llu bP points : 100%%     \n", (unsigned long long)ext, (unsigned long long)ext);
+    if (!(have & kFileBp)) printf("[+] Sorting %llu elements... Done!\n", (unsigned long long)geo.m3);
+  } else if (!T.build(geo, nthreads, 4, err, nullptr, have)) {   // giant tables + lane offsets only
     fprintf(stderr, "%s\n", err.c_str());
     exit(EXIT_FAILURE);
   }
-  printf("\r[+] processing %llu/%llu bP points : 100%%     \n", (unsigned long long)geo.l1ext,
-         (unsigned long long)geo.l1ext);
-  printf("[+] Sorting %llu elements... Done!\n", (unsigned long long)geo.m3);
+  if (save_read_file && have != kFileAll && !T.save_files(".", have, err, say)) {   // keyhunt.cpp:1881-2025
+    fprintf(stderr, "%s\n", err.c_str());
+    exit(EXIT_FAILURE);
+  }
 
   // ---- search
   std::mutex out_mu;

@@ -45,6 +45,35 @@ khh_tables* khh_tables_new(const char* n_str, int k, int threads, uint32_t gpl, 
   return t;
 }
 
+khh_tables* khh_tables_new_files(const char* n_str, int k, int threads, uint32_t gpl, const char* dir,
+                                 int skip_checksum, int save, uint32_t* have, char* err, size_t errlen) {
+  Geometry g;
+  std::string e;
+  if (!make_geometry(n_str, k, g, e)) { set_err(err, errlen, e); return nullptr; }
+  khh_tables* t = new khh_tables();
+  if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
+  uint32_t h = 0;
+  t->t.prepare(g);
+  if (!t->t.load_files(dir ? dir : ".", skip_checksum != 0, h, e, nullptr) ||
+      !t->t.build(g, threads, gpl ? gpl : 4, e, nullptr, h) ||
+      (save && h != kFileAll && !t->t.save_files(dir ? dir : ".", h, e, nullptr))) {
+    set_err(err, errlen, e);
+    delete t;
+    return nullptr;
+  }
+  if (have) *have = h;
+  return t;
+}
+
+int khh_tables_save(const khh_tables* t, const char* dir, char* err, size_t errlen) {
+  std::string e;
+  if (!t->t.save_files(dir ? dir : ".", 0, e, nullptr)) {
+    set_err(err, errlen, e);
+    return -100;
+  }
+  return 0;
+}
+
 void khh_tables_free(khh_tables* t) { delete t; }
 
 void khh_params(const khh_tables* t, uint64_t out[10]) {

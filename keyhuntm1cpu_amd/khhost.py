@@ -26,6 +26,10 @@ def lib() -> C.CDLL:
         L.khh_tables_new.restype = C.c_void_p
         L.khh_tables_new.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_uint32, C.c_char_p, C.c_size_t]
         L.khh_tables_free.argtypes = [C.c_void_p]
+        L.khh_tables_new_files.restype = C.c_void_p
+        L.khh_tables_new_files.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_uint32, C.c_char_p, C.c_int, C.c_int,
+                                           P(C.c_uint32), C.c_char_p, C.c_size_t]
+        L.khh_tables_save.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t]
         L.khh_params.argtypes = [C.c_void_p, P(C.c_uint64)]
         L.khh_bloom.restype = P(C.c_uint8)
         L.khh_bloom.argtypes = [C.c_void_p, C.c_int, C.c_int, P(C.c_uint64), P(C.c_uint64), P(C.c_uint32)]
@@ -90,9 +94,19 @@ def parse_pubkey(s: str) -> tuple[bytes, bool] | None:
 class Tables:
     """keyhunt's BSGS tables built by the product host engine."""
 
-    def __init__(self, n: str | None = None, k: int = 1, threads: int = 0, gpl: int = 4):
+    def __init__(self, n: str | None = None, k: int = 1, threads: int = 0, gpl: int = 4,
+                 files_dir: str | None = None, save: bool = False, skip_checksum: bool = False):
+        """files_dir: -S semantics — read the reference's table files from that directory, compute
+        only what is missing, and with save=True write the missing files back (self.have = mask)."""
         err = C.create_string_buffer(256)
-        self.h = lib().khh_tables_new(n.encode() if n else None, k, threads, gpl, err, 256)
+        self.have = 0
+        if files_dir is not None:
+            have = C.c_uint32(0)
+            self.h = lib().khh_tables_new_files(n.encode() if n else None, k, threads, gpl, files_dir.encode(),
+                                                1 if skip_checksum else 0, 1 if save else 0, C.byref(have), err, 256)
+            self.have = int(have.value)
+        else:
+            self.h = lib().khh_tables_new(n.encode() if n else None, k, threads, gpl, err, 256)
         if not self.h:
             raise KhhError(err.value.decode())
         p = (C.c_uint64 * 10)()
@@ -110,6 +124,11 @@ class Tables:
             self.close()
         except Exception:
             pass
+
+    def save_files(self, directory: str) -> None:
+        err = C.create_string_buffer(256)
+        if lib().khh_tables_save(self.h, directory.encode(), err, 256):
+            raise KhhError(err.value.decode())
 
     def bloom(self, level: int, idx: int) -> tuple[bytes, int, int]:
         nb, bits, h = C.c_uint64(), C.c_uint64(), C.c_uint32()

@@ -171,3 +171,22 @@ def test_k4_synthetic_key_search(tables_k4):
     res, st = tables_k4.search([xy], 1 << 65, (1 << 65) + (1 << 47))
     assert res == [d]
     assert st["chunks"] <= 4
+
+
+def test_cli_save_read_table_files(tmp_path):
+    """-S: the first run writes keyhunt_bsgs_{4,6,2,7}_* in the working directory, the second reads
+    them (no baby-step work) and finds the same key (keyhunt.cpp:1373-1613, 1881-2025)."""
+    p30 = "030d282cf2ff536d2c42f105d0b8588821a915dc3f9a05bd98bb23af67a2e92a5b"
+    (tmp_path / "30.pub").write_text(p30 + "\n")
+    args = ["-m", "bsgs", "-f", "30.pub", "-b", "30", "-n", "0x100000", "-S", "-q", "-s", "0"]
+    r1 = _cli(args, tmp_path)
+    assert r1.returncode == 1, r1.stdout + r1.stderr
+    assert "[+] Writing bloom filter to file keyhunt_bsgs_4_1024.blm" in r1.stdout
+    assert "[+] Writing bP Table to file keyhunt_bsgs_2_1.tbl" in r1.stdout
+    assert "privkey 3d94cd64" in r1.stdout
+    r2 = _cli(args, tmp_path)
+    assert r2.returncode == 1, r2.stdout + r2.stderr
+    assert "[+] Reading bloom filter from file keyhunt_bsgs_4_1024.blm" in r2.stdout
+    assert "[+] Reading bP Table from file keyhunt_bsgs_2_1.tbl" in r2.stdout
+    assert "Writing" not in r2.stdout
+    assert "privkey 3d94cd64" in r2.stdout
