@@ -142,6 +142,19 @@ int khb_addr_dump(khb_ctx* ctx, const uint8_t* centre_xy_be, uint32_t group_begi
  * bloom_check20 result against the loaded address bloom (0 when none is loaded). */
 int khb_hash160(khb_ctx* ctx, int kind, const uint8_t* xy_be, uint8_t* out, uint32_t n);
 
+/* ---- baby-step tables on the GPU (thread_bPload, keyhunt.cpp:4404-4592; orchestration 1615-1880) ----
+ * Uses the loaded giant table as Gn[i] = (i+1)*G, _2Gn = 1024*G and the lane offsets for jobs of
+ * groups_per_job groups.  Job k covers baby steps ic = k*groups_per_job*1024 + [0, groups_per_job*1024)
+ * (key ic + 1); centres[k] = pubkey(k*groups_per_job*1024 + 513).  Every x with ic < l1ext is added
+ * to the level-1 bloom, ic < m2 to level 2, ic < m3 to level 3 and written to bp as struct
+ * bsgs_xvalue {x bytes 16..21, 2 zero bytes, u64 ic} (unsorted).  l1/l2/l3 receive 256 concatenated
+ * sub-blooms of bytes_per_sub[level] bytes (NULL skips a level, e.g. one read from -S files);
+ * bp receives m3*16 bytes (NULL skips it). */
+int khb_build_baby(khb_ctx* ctx, const uint8_t* centres_xy_be, uint32_t n_jobs, uint32_t groups_per_job,
+                   uint64_t l1ext, uint64_t m2, uint64_t m3, const uint64_t bytes_per_sub[3],
+                   const uint64_t bits_per_sub[3], const uint32_t hashes[3], uint8_t* l1, uint8_t* l2, uint8_t* l3,
+                   uint8_t* bp, float* kernel_ms);
+
 #ifdef __cplusplus
 }
 #endif

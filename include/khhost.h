@@ -29,6 +29,10 @@ void khh_tables_free(khh_tables* t);
  * are written back.  *have receives the mask of files read (1 L1, 2 L2, 4 bPtable, 8 L3). */
 khh_tables* khh_tables_new_files(const char* n_str, int k, int threads, uint32_t gpl, const char* dir,
                                  int skip_checksum, int save, uint32_t* have, char* err, size_t errlen);
+/* Like khh_tables_new with the baby-step walk on GPU `device` (khb_build_baby); identical tables.
+ * *kernel_ms (nullable) receives the build kernel's time. */
+khh_tables* khh_tables_new_gpu(const char* n_str, int k, int threads, uint32_t gpl, int device, double* kernel_ms,
+                               char* err, size_t errlen);
 /* Write all four table files into dir. */
 int khh_tables_save(const khh_tables* t, const char* dir, char* err, size_t errlen);
 /* out: [0]=m [1]=m2 [2]=m3 [3]=aux [4]=cycles [5]=N(low64) [6]=l1 extent [7..9]=bloom entries L1..L3 */

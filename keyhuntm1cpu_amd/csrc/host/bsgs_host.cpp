@@ -1,5 +1,7 @@
 #include "bsgs_host.hpp"
 
+#include "../../../include/khbsgs.h"
+
 #include <string.h>
 
 #include <algorithm>
@@ -120,6 +122,60 @@ bool make_geometry(const char* n_str, int kfactor, Geometry& g, std::string& err
   return true;
 }
 
+// Baby-step walk on the GPU (khb_build_baby): jobs of 2^20 keys, centre key k*2^20 + 513.
+static bool build_baby_gpu(Tables& T, const Geometry& g, const std::vector<Pt>& gn, const Pt& g2n, uint64_t extent,
+                           bool need_l1, bool need_l2, bool need_l3, bool need_bp, int device, int nthreads,
+                           double& kernel_ms, std::string& err) {
+  const uint32_t gpj = 1024, gpl = 4;
+  const uint64_t job_keys = (uint64_t)gpj * kGrp;
+  const uint32_t n_jobs = (uint32_t)((extent + job_keys - 1) / job_keys);
+  std::vector<uint8_t> centres(64 * (size_t)n_jobs), tab(513 * 64), offs(64 * (gpj / gpl));
+  {
+    std::atomic<uint32_t> next{0};
+    auto work = [&] {
+      for (uint32_t k; (k = next.fetch_add(1)) < n_jobs;)
+        pt_to_be(centres.data() + 64 * (size_t)k, mul_g(U256((uint64_t)k * job_keys + 1 + kHalf)));
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+  }
+  for (int i = 0; i < kHalf; ++i) pt_to_be(tab.data() + 64 * i, gn[i]);
+  pt_to_be(tab.data() + 64 * kHalf, g2n);
+  for (uint32_t m = 1; m < gpj / gpl; ++m) pt_to_be(offs.data() + 64 * m, mul_g(U256((uint64_t)m * gpl * kGrp)));
+  khb_ctx* ctx = nullptr;
+  int rc = khb_open(device, 0, &ctx);
+  if (rc) {
+    err = std::string("[E] GPU table build: ") + khb_strerror(rc);
+    return false;
+  }
+  const uint64_t bytes[3] = {T.l1[0].bytes, T.l2[0].bytes, T.l3[0].bytes};
+  const uint64_t bits[3] = {T.l1[0].bits, T.l2[0].bits, T.l3[0].bits};
+  const uint32_t hashes[3] = {T.l1[0].hashes, T.l2[0].hashes, T.l3[0].hashes};
+  std::vector<uint8_t> cat[3];
+  if (need_l1) cat[0].assign(256 * bytes[0], 0);
+  if (need_l2) cat[1].assign(256 * bytes[1], 0);
+  if (need_l3) cat[2].assign(256 * bytes[2], 0);
+  float ms = 0;
+  if (!(rc = khb_load_giant_table(ctx, tab.data())) &&
+      !(rc = khb_load_lane_offsets(ctx, offs.data(), gpj / gpl, gpl)))
+    rc = khb_build_baby(ctx, centres.data(), n_jobs, gpj, g.l1ext, g.m2, g.m3, bytes, bits, hashes,
+                        need_l1 ? cat[0].data() : nullptr, need_l2 ? cat[1].data() : nullptr,
+                        need_l3 ? cat[2].data() : nullptr, need_bp ? (uint8_t*)T.bp.data() : nullptr, &ms);
+  khb_close(ctx);
+  if (rc) {
+    err = std::string("[E] GPU table build: ") + khb_strerror(rc);
+    return false;
+  }
+  kernel_ms = ms;
+  std::vector<BloomFilter>* lv[3] = {&T.l1, &T.l2, &T.l3};
+  for (int l = 0; l < 3; ++l)
+    if (!cat[l].empty())
+      for (int i = 0; i < 256; ++i) memcpy((*lv[l])[i].bf.data(), cat[l].data() + i * bytes[l], bytes[l]);
+  return true;
+}
+
 void Tables::prepare(const Geometry& g) {
   geo = g;
   l1.assign(256, BloomFilter());
@@ -129,7 +185,7 @@ void Tables::prepare(const Geometry& g) {
 }
 
 bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, std::string& err,
-                   const std::function<void(uint64_t, uint64_t)>& progress, uint32_t have) {
+                   const std::function<void(uint64_t, uint64_t)>& progress, uint32_t have, int gpu_device) {
   if (!have) prepare(g);
   geo = g;
   for (int i = 0; i < 256; ++i) {
@@ -191,6 +247,13 @@ bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, st
     }
   }
   if (nthreads < 1) nthreads = 1;
+  if (gpu_device >= 0 && extent) {
+    if (!build_baby_gpu(*this, g, gn, g2n, extent, need_l1, need_l2, need_l3, need_bp, gpu_device, nthreads,
+                        build_gpu_ms, err))
+      return false;
+    jobs.clear();   // the CPU workers below only compute the lane offsets
+    if (progress) progress(extent, extent);
+  }
   std::atomic<uint64_t> next_job{0}, next_off{1}, done{0};
   std::atomic<int> finished{0};
   auto worker = [&]() {

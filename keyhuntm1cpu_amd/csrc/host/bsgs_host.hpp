@@ -50,8 +50,11 @@ struct Tables {
   // progress(done, total) is called from the builder threads' coordinator.  `have` marks tables
   // already loaded from -S files (load_files): their baby-step work is skipped, and with L1 loaded
   // only the first m2 baby steps are walked (keyhunt.cpp:1617-1700, "only 3% of the work").
+  // gpu_device >= 0 walks the baby steps on that GPU (khb_build_baby); the tables are identical.
   bool build(const Geometry& g, int nthreads, uint32_t groups_per_lane, std::string& err,
-             const std::function<void(uint64_t, uint64_t)>& progress = nullptr, uint32_t have = 0);
+             const std::function<void(uint64_t, uint64_t)>& progress = nullptr, uint32_t have = 0,
+             int gpu_device = -1);
+  double build_gpu_ms = 0;               // kernel time of the last GPU baby-step build
   // -S: read the reference's table files for this geometry from dir (prepare() first).  Returns the
   // kFile* mask read; false + err on a short read or checksum mismatch (the reference exits).
   void prepare(const Geometry& g);

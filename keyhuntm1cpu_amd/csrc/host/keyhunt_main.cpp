@@ -50,6 +50,7 @@ void menu() {
   printf("-R          Random, this is the default behavior\n");
   printf("-s ns       Number of seconds for the stats output, 0 to omit output.\n");
   printf("-t tn       CPU threads for table build and candidate confirmation\n");
+  printf("--cpu-build build the baby-step tables on the CPU (default: on the first GPU)\n");
   printf("-6          to skip sha256 Checksum on data files\n");
   printf("--gpu       use the GPU path (always on: keyhunt_amd has no CPU giant-step path)\n");
   printf("-g ids      GPU device ids, comma separated (default 0)\n");
@@ -152,7 +153,7 @@ int main(int argc, char** argv) {
   SearchConfig cfg;
   uint32_t gpu_blocks = 0;
   AddressCli ao;
-  bool save_read_file = false, skip_checksum = false;
+  bool save_read_file = false, skip_checksum = false, cpu_build = false;
   bool endomorphism = false, eth = false;
   const char* kSearch[3] = {"uncompress", "compress", "both"};   // keyhunt.cpp:230
   if (nthreads > 16) nthreads = 16;
@@ -160,6 +161,7 @@ int main(int argc, char** argv) {
                                      {"gpu-threads", required_argument, nullptr, 1001},
                                      {"gpu-blocks", required_argument, nullptr, 1002},
                                      {"max-chunks", required_argument, nullptr, 1003},
+                                     {"cpu-build", no_argument, nullptr, 1004},
                                      {nullptr, 0, nullptr, 0}};
   int c;
   while ((c = getopt_long(argc, argv, "deh6MqRSB:b:c:C:E:f:I:k:l:m:N:n:p:r:s:t:v:G:8:z:g:", longopts, nullptr)) != -1) {
@@ -256,6 +258,7 @@ int main(int argc, char** argv) {
       case 1001: break;                             // --gpu-threads: fixed 256-lane workgroups
       case 1002: gpu_blocks = (uint32_t)strtoul(optarg, nullptr, 10); break;
       case 1003: cfg.max_chunks = strtoull(optarg, nullptr, 10); break;
+      case 1004: cpu_build = true; break;
       case 'C': case 'E': case 'N': case 'p': case 'v': case 'G': case '8': case 'z':
         break;   // options of the other search modes
       default:
@@ -429,11 +432,12 @@ int main(int argc, char** argv) {
       printf("[I] We need to recalculate some files, don't worry this is only 3%% of the previous work\n");
   }
   if (have != kFileAll || !save_read_file) {
+    // baby steps on the first GPU unless --cpu-build (identical tables; tests/test_gpu_tables.py)
     if (!T.build(geo, nthreads, 4, err, [&](uint64_t d, uint64_t tot) {
           printf("\r[+] processing %llu/%llu bP points : %i%%\r", (unsigned long long)d, (unsigned long long)tot,
                  (int)((double)d / (double)tot * 100));
           fflush(stdout);
-        }, have)) {
+        }, have, cpu_build ? -1 : cfg.devices[0])) {
       fprintf(stderr, "%s\n", err.c_str());
       exit(EXIT_FAILURE);
     }

@@ -65,6 +65,22 @@ khh_tables* khh_tables_new_files(const char* n_str, int k, int threads, uint32_t
   return t;
 }
 
+khh_tables* khh_tables_new_gpu(const char* n_str, int k, int threads, uint32_t gpl, int device, double* kernel_ms,
+                               char* err, size_t errlen) {
+  Geometry g;
+  std::string e;
+  if (!make_geometry(n_str, k, g, e)) { set_err(err, errlen, e); return nullptr; }
+  khh_tables* t = new khh_tables();
+  if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
+  if (!t->t.build(g, threads, gpl ? gpl : 4, e, nullptr, 0, device)) {
+    set_err(err, errlen, e);
+    delete t;
+    return nullptr;
+  }
+  if (kernel_ms) *kernel_ms = t->t.build_gpu_ms;
+  return t;
+}
+
 int khh_tables_save(const khh_tables* t, const char* dir, char* err, size_t errlen) {
   std::string e;
   if (!t->t.save_files(dir ? dir : ".", 0, e, nullptr)) {

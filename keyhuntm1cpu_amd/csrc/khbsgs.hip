@@ -53,10 +53,11 @@ enum : int {
   kAddrC = 3,      // -m address, -l compress
   kAddrB = 4,      // -m address, -l both (the reference default, keyhunt.cpp:300)
   kAddrDump = 5,   // -m address parity: write every x||y
+  kBaby = 6,       // baby-step table build: bloom_add of every x into L1/L2/L3 + bPtable records
 };
-constexpr bool is_addr(int m) { return m >= kAddrU; }
+constexpr bool is_addr(int m) { return m >= kAddrU && m <= kAddrDump; }
 constexpr bool needs_y(int m) { return m == kAddrU || m == kAddrB || m == kAddrDump; }
-constexpr bool is_dump(int m) { return m == kDump || m == kAddrDump; }
+constexpr bool is_dump(int m) { return m == kDump || m == kAddrDump || m == kBaby; }
 constexpr uint32_t kHalf = KHB_GROUP / 2;            // 512
 constexpr uint32_t kCandCap = 1u << 20;
 constexpr uint32_t kAddrHitCap = 1u << 18;
@@ -75,6 +76,13 @@ struct ScanArgs {
   uint8_t* __restrict__ xdump;         // dump modes only
   uint32_t* __restrict__ ahits;        // -m address hits: {job, group, t, kind} x ahit_cap
   uint32_t ahit_cap;
+  // kBaby: word-aligned blooms (sub-bloom stride bwords[l] 32-bit words; null = level skipped)
+  uint32_t* __restrict__ bw[3];
+  BloomGeom bgeom[3];
+  uint64_t bwords[3];
+  uint64_t blimit[3];                  // ic < blimit[l] goes into level l (l1ext, m2, m3)
+  uint32_t* __restrict__ bp;           // m3 x 16-byte struct bsgs_xvalue records (null = skipped)
+  uint64_t job_keys;                   // baby steps per job
   uint64_t n_items;
   uint32_t n_jobs, group_begin, group_end, gpl, lanes_per_job, stride, cand_cap, degen_cap;
 };
@@ -294,6 +302,48 @@ __device__ __forceinline__ void addr_point(const ScanArgs& A, const Fe& x, const
   }
 }
 
+// bloom_add (bloom.cpp:61-85, 159-162) of a 32-byte x into sub-bloom x[0] of a word-aligned level.
+__device__ __forceinline__ void bloom_add_words(uint32_t* __restrict__ words, const BloomGeom& g, uint64_t a,
+                                                uint64_t b) {
+  uint64_t pos = mod_bits(a, g);
+  const uint64_t bm = mod_bits(b, g);
+  uint64_t h = a;
+  for (uint32_t i = 0; i < g.hashes; ++i) {
+    if (i) {
+      const uint64_t nh = h + b;
+      const bool wrapped = nh < h;
+      h = nh;
+      pos += bm;
+      if (pos >= g.bits) pos -= g.bits;
+      if (wrapped) pos = (pos >= g.wrap) ? pos - g.wrap : pos + g.bits - g.wrap;
+    }
+    // bf[pos >> 3] |= 1 << (pos & 7): little-endian words, so bit (pos & 31) of word pos >> 5
+    atomicOr(words + (pos >> 5), 1u << (pos & 31));
+  }
+}
+
+// Baby step ic = job * job_keys + 1024 j + t (key ic + 1): thread_bPload (keyhunt.cpp:4404-4592).
+__device__ __forceinline__ void baby_point(const ScanArgs& A, const Fe& x, uint32_t job, uint32_t j, uint32_t t) {
+  const uint64_t ic = (uint64_t)job * A.job_keys + (uint64_t)j * KHB_GROUP + t;
+  if (ic >= A.blimit[0] && ic >= A.blimit[1] && ic >= A.blimit[2]) return;
+  uint64_t w[4];
+  x_words(w, x);
+  const uint64_t a = xxh64_32(w, KHB_BLOOM_SEED);
+  const uint64_t b = xxh64_32(w, a);
+  const uint32_t sub = x.v[7] >> 24;
+#pragma unroll 1
+  for (int l = 0; l < 3; ++l)
+    if (A.bw[l] && ic < A.blimit[l]) bloom_add_words(A.bw[l] + sub * A.bwords[l], A.bgeom[l], a, b);
+  if (A.bp && ic < A.blimit[2]) {
+    // struct bsgs_xvalue {value = x bytes 16..21 (Get32Bytes order), pad[2] = 0, index = ic}
+    uint32_t* o = A.bp + 4 * ic;
+    o[0] = __builtin_bswap32(x.v[3]);
+    o[1] = (x.v[2] >> 24) | (((x.v[2] >> 16) & 0xffu) << 8);
+    o[2] = (uint32_t)ic;
+    o[3] = (uint32_t)(ic >> 32);
+  }
+}
+
 // One reference group centred on C; advances C to the next centre.  For -m bsgs this is
 // keyhunt.cpp:3873-3999 (table GSn, x only); for -m address it is keyhunt.cpp:2586-2711 with the
 // table Gn (same point order t = 0..1023, pts[t] = key + t), plus y where the search needs it.
@@ -378,7 +428,10 @@ __device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, Aff
       fm_sqr(x2, s);
       fm_sub(x2, x2, u);
       fm_canon(x2, x2);
-      if constexpr (is_addr(MODE)) {
+      if constexpr (MODE == kBaby) {
+        baby_point(A, x1, job, j, kHalf - 1 - (uint32_t)i);
+        baby_point(A, x2, job, j, kHalf + 1 + (uint32_t)i);
+      } else if constexpr (is_addr(MODE)) {
         if constexpr (needs_y(MODE)) {
           fm_sub(y2, g.x, x2);
           fm_mul(y2, y2, s);
@@ -391,13 +444,17 @@ __device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, Aff
         probe_pair<DUMP>(A, Q, x1, x2, job, j, kHalf - 1 - (uint32_t)i, kHalf + 1 + (uint32_t)i);
       }
     } else {
-      if constexpr (is_addr(MODE))
+      if constexpr (MODE == kBaby)
+        baby_point(A, x1, job, j, kHalf - 1 - (uint32_t)i);
+      else if constexpr (is_addr(MODE))
         addr_point<MODE>(A, x1, y1, job, j, kHalf - 1 - (uint32_t)i);
       else
         probe<DUMP>(A, Q, x1, job, j, kHalf - 1 - (uint32_t)i);
     }
   }
-  if constexpr (is_addr(MODE))
+  if constexpr (MODE == kBaby)
+    baby_point(A, C.x, job, j, kHalf);
+  else if constexpr (is_addr(MODE))
     addr_point<MODE>(A, C.x, C.y, job, j, kHalf);
   else
     probe<DUMP>(A, Q, C.x, job, j, kHalf);
@@ -996,6 +1053,81 @@ int khb_hash160(khb_ctx* c, int kind, const uint8_t* xy, uint8_t* out, uint32_t 
   hipFree(d);
   hipFree(dout);
   free(h);
+  if (e != hipSuccess) return hip_fail(c, e);
+  return KHB_OK;
+}
+
+
+// ------------------------------------------------------------------------- baby-step tables
+int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t groups_per_job, uint64_t l1ext,
+                   uint64_t m2, uint64_t m3, const uint64_t bytes_per_sub[3], const uint64_t bits_per_sub[3],
+                   const uint32_t hashes[3], uint8_t* l1, uint8_t* l2, uint8_t* l3, uint8_t* bp, float* kernel_ms) {
+  int rc = check_scan_args(c, centres, n_jobs, 0, groups_per_job, false);
+  if (rc) return rc;
+  if (!bytes_per_sub || !bits_per_sub || !hashes) return KHB_EINVAL;
+  uint8_t* outs[3] = {l1, l2, l3};
+  for (int l = 0; l < 3; ++l)
+    if (outs[l] && (bits_per_sub[l] < 2 || (bits_per_sub[l] + 7) / 8 != bytes_per_sub[l] || hashes[l] == 0 ||
+                    hashes[l] > 255))
+      return KHB_EINVAL;
+  if (c->in_flight || c->addr_in_flight) return KHB_EBUSY;
+  KHB_TRY(c, hipSetDevice(c->device));
+  if ((rc = ensure_centres(c, n_jobs))) return rc;
+  pts_from_be(c->h_centres, centres, n_jobs);
+  ScanArgs A = make_args(c, n_jobs, 0, groups_per_job);
+  A.job_keys = (uint64_t)groups_per_job * KHB_GROUP;
+  A.blimit[0] = l1 ? l1ext : 0;
+  A.blimit[1] = l2 ? m2 : 0;
+  A.blimit[2] = (l3 || bp) ? m3 : 0;
+  uint32_t* dw[3] = {nullptr, nullptr, nullptr};
+  uint32_t* dbp = nullptr;
+  hipError_t e = hipSuccess;
+  for (int l = 0; l < 3 && e == hipSuccess; ++l) {
+    if (!outs[l]) continue;
+    const uint64_t words = (bytes_per_sub[l] + 3) / 4;
+    e = hipMalloc(&dw[l], 256 * words * 4);
+    if (e == hipSuccess) e = hipMemsetAsync(dw[l], 0, 256 * words * 4, c->stream);
+    A.bw[l] = dw[l];
+    A.bwords[l] = words;
+    BloomGeom& g = A.bgeom[l];
+    g.bytes_per_sub = bytes_per_sub[l];
+    g.bits = bits_per_sub[l];
+    g.magic = (uint64_t)(((unsigned __int128)1 << 64) / g.bits);
+    g.wrap = (uint64_t)(((unsigned __int128)1 << 64) % g.bits);
+    g.hashes = hashes[l];
+  }
+  if (e == hipSuccess && bp && m3) {
+    e = hipMalloc(&dbp, 16 * m3);
+    A.bp = dbp;
+  }
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, 16, c->stream);
+  if (e == hipSuccess) e = hipEventRecord(c->ev0, c->stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_giant_scan<kBaby>, dim3(c->lanes / kBlock), dim3(kBlock), 0, c->stream, A);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipEventRecord(c->ev1, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess && kernel_ms) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) ms = -1.f;
+    *kernel_ms = ms;
+  }
+  for (int l = 0; l < 3 && e == hipSuccess; ++l) {
+    if (!outs[l]) continue;
+    const uint64_t words = A.bwords[l], nb = bytes_per_sub[l];
+    uint8_t* tmp = (uint8_t*)malloc(256 * words * 4);
+    if (!tmp) { e = hipErrorOutOfMemory; break; }
+    e = hipMemcpy(tmp, dw[l], 256 * words * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess)
+      for (int sub = 0; sub < 256; ++sub) memcpy(outs[l] + sub * nb, tmp + sub * words * 4, nb);
+    free(tmp);
+  }
+  if (e == hipSuccess && dbp) e = hipMemcpy(bp, dbp, 16 * m3, hipMemcpyDeviceToHost);
+  for (int l = 0; l < 3; ++l) hipFree(dw[l]);
+  hipFree(dbp);
   if (e != hipSuccess) return hip_fail(c, e);
   return KHB_OK;
 }

@@ -30,6 +30,9 @@ def lib() -> C.CDLL:
         L.khh_tables_new_files.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_uint32, C.c_char_p, C.c_int, C.c_int,
                                            P(C.c_uint32), C.c_char_p, C.c_size_t]
         L.khh_tables_save.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t]
+        L.khh_tables_new_gpu.restype = C.c_void_p
+        L.khh_tables_new_gpu.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_uint32, C.c_int, P(C.c_double), C.c_char_p,
+                                         C.c_size_t]
         L.khh_params.argtypes = [C.c_void_p, P(C.c_uint64)]
         L.khh_bloom.restype = P(C.c_uint8)
         L.khh_bloom.argtypes = [C.c_void_p, C.c_int, C.c_int, P(C.c_uint64), P(C.c_uint64), P(C.c_uint32)]
@@ -95,12 +98,19 @@ class Tables:
     """keyhunt's BSGS tables built by the product host engine."""
 
     def __init__(self, n: str | None = None, k: int = 1, threads: int = 0, gpl: int = 4,
-                 files_dir: str | None = None, save: bool = False, skip_checksum: bool = False):
+                 files_dir: str | None = None, save: bool = False, skip_checksum: bool = False,
+                 gpu_device: int | None = None):
         """files_dir: -S semantics — read the reference's table files from that directory, compute
         only what is missing, and with save=True write the missing files back (self.have = mask)."""
         err = C.create_string_buffer(256)
         self.have = 0
-        if files_dir is not None:
+        self.build_ms = 0.0
+        if gpu_device is not None:
+            ms = C.c_double(0)
+            self.h = lib().khh_tables_new_gpu(n.encode() if n else None, k, threads, gpl, gpu_device, C.byref(ms),
+                                              err, 256)
+            self.build_ms = ms.value
+        elif files_dir is not None:
             have = C.c_uint32(0)
             self.h = lib().khh_tables_new_files(n.encode() if n else None, k, threads, gpl, files_dir.encode(),
                                                 1 if skip_checksum else 0, 1 if save else 0, C.byref(have), err, 256)
