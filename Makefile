@@ -1,7 +1,8 @@
 # Build everything in-tree (the .so / binaries travel to the GPU box with the repo snapshot).
 #   keyhuntm1cpu_amd/lib/libkhbsgs.so   HIP giant-step library (gfx950), include/khbsgs.h
 #   keyhuntm1cpu_amd/lib/libkhhost.so   C++ host engine, include/khhost.h
-#   keyhuntm1cpu_amd/bin/keyhunt_amd    keyhunt-compatible CLI (-m bsgs)
+#   keyhuntm1cpu_amd/bin/keyhunt_amd    keyhunt-compatible CLI (-m bsgs, -m address, -m rmd160)
+#   keyhuntm1cpu_amd/bin/bsgsd_amd      bsgsd-compatible TCP daemon
 #   oracle/build/liboracle.so           test-only checker (oracle/Makefile)
 HIPCC    ?= /opt/rocm/bin/hipcc
 CXX      ?= g++
@@ -20,7 +21,7 @@ HOST_SRCS := $(CSRC)/host/u256.cpp $(CSRC)/host/secp_host.cpp $(CSRC)/host/bloom
 HOST_HDRS := $(wildcard $(CSRC)/host/*.hpp) $(DEV_HDRS) include/khhost.h
 HOST_OBJS := $(patsubst $(CSRC)/host/%.cpp,build/host/%.o,$(HOST_SRCS))
 
-all: $(LIBDIR)/libkhbsgs.so $(LIBDIR)/libkhhost.so $(BINDIR)/keyhunt_amd oracle
+all: $(LIBDIR)/libkhbsgs.so $(LIBDIR)/libkhhost.so $(BINDIR)/keyhunt_amd $(BINDIR)/bsgsd_amd oracle
 
 $(LIBDIR) $(BINDIR) build/host:
 	mkdir -p $@
@@ -37,6 +38,9 @@ $(LIBDIR)/libkhhost.so: $(HOST_OBJS) build/host/khhost_capi.o $(LIBDIR)/libkhbsg
 CLI_OBJS := build/host/keyhunt_main.o build/host/keyhunt_address.o
 $(BINDIR)/keyhunt_amd: $(HOST_OBJS) $(CLI_OBJS) $(LIBDIR)/libkhbsgs.so | $(BINDIR)
 	$(CXX) $(CXXFLAGS) -o $@ $(HOST_OBJS) $(CLI_OBJS) -L$(LIBDIR) -lkhbsgs -Wl,-rpath,'$$ORIGIN/../lib'
+
+$(BINDIR)/bsgsd_amd: $(HOST_OBJS) build/host/bsgsd_main.o $(LIBDIR)/libkhbsgs.so | $(BINDIR)
+	$(CXX) $(CXXFLAGS) -o $@ $(HOST_OBJS) build/host/bsgsd_main.o -L$(LIBDIR) -lkhbsgs -Wl,-rpath,'$$ORIGIN/../lib'
 
 oracle:
 	$(MAKE) -s -C oracle
