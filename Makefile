@@ -51,7 +51,7 @@ clean:
 .PHONY: all oracle clean
 
 # Kernel variants for A/B timing (tools/perf_variants.py); not used by the product.
-VARIANTS := w2 g0
+VARIANTS := r2
 variants: $(patsubst %,$(LIBDIR)/variants/libkhbsgs_%.so,$(VARIANTS))
 $(LIBDIR)/variants/libkhbsgs_w%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
@@ -71,9 +71,6 @@ $(LIBDIR)/variants/libkhbsgs_m1s%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 $(LIBDIR)/variants/libkhbsgs_m2s%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) -DKHB_MUL_IMPL=2 -DKHB_SQR_IMPL=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_d%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
-	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_DRAIN_WIDTH=$* -DKHB_PROBE_BITS=1 -shared -o $@ $(CSRC)/khbsgs.hip
 $(LIBDIR)/variants/libkhbsgs_p%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) -DKHB_PROBE_MODE=$* -shared -o $@ $(CSRC)/khbsgs.hip

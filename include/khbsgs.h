@@ -79,6 +79,13 @@ uint32_t khb_lanes(const khb_ctx* ctx);
  * (bloom_bP[0..255].bf, bloom.h:26-45).  bits/hashes as in struct bloom. */
 int khb_load_bloom(khb_ctx* ctx, const uint8_t* bf_concat, uint64_t bytes_per_sub, uint64_t bits_per_sub,
                    uint32_t hashes);
+/* Level-0 gate in front of the level-1 probe (no reference counterpart; a superset filter): a map of
+ * 2^log2_bits bits, bit (XXH64(x, seed) >> (64 - log2_bits)) set for every baby-step x of the level-1
+ * set (bit i of byte i/8, LSB first; khb_build_baby writes one).  With a gate, the giant-step probe
+ * reads the gate bit first and runs the level-1 check only when it is set: every level-1 candidate
+ * whose gate bit is set is still reported, so no baby-step hit is lost.  gate NULL removes it;
+ * log2_bits in [13, 40]. */
+int khb_load_gate(khb_ctx* ctx, const uint8_t* gate, uint32_t log2_bits);
 /* GSn[0..511] and _2GSn (keyhunt.cpp:1325-1338), 513 affine points x||y BE. */
 int khb_load_giant_table(khb_ctx* ctx, const uint8_t* gsn_xy_be);
 /* Lane start offsets: offs[m] = (m*groups_per_lane) * _2GSn, m in [0, n) (offs[0] unused: the
@@ -149,11 +156,12 @@ int khb_hash160(khb_ctx* ctx, int kind, const uint8_t* xy_be, uint8_t* out, uint
  * to the level-1 bloom, ic < m2 to level 2, ic < m3 to level 3 and written to bp as struct
  * bsgs_xvalue {x bytes 16..21, 2 zero bytes, u64 ic} (unsorted).  l1/l2/l3 receive 256 concatenated
  * sub-blooms of bytes_per_sub[level] bytes (NULL skips a level, e.g. one read from -S files);
- * bp receives m3*16 bytes (NULL skips it). */
+ * bp receives m3*16 bytes (NULL skips it).  gate (NULL skips it) receives the level-0 gate of
+ * khb_load_gate for every ic < l1ext, 2^gate_log2 bits. */
 int khb_build_baby(khb_ctx* ctx, const uint8_t* centres_xy_be, uint32_t n_jobs, uint32_t groups_per_job,
                    uint64_t l1ext, uint64_t m2, uint64_t m3, const uint64_t bytes_per_sub[3],
                    const uint64_t bits_per_sub[3], const uint32_t hashes[3], uint8_t* l1, uint8_t* l2, uint8_t* l3,
-                   uint8_t* bp, float* kernel_ms);
+                   uint8_t* bp, uint8_t* gate, uint32_t gate_log2, float* kernel_ms);
 
 #ifdef __cplusplus
 }

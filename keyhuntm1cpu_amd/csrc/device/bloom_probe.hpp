@@ -124,33 +124,15 @@ KHB_HD bool bloom_rest_r(const uint8_t* __restrict__ bf, const BloomGeom& g, con
   return bloom_steps<R>(bf, g, a, xxh64_32(w, a));
 }
 
-// bloom_rest for two independent x at once (ok1/ok2 in: entry valid, out: all bits set).  Each
-// round fetches the next bit of both live entries, so one memory round trip serves both.
-KHB_HD void bloom_rest_pair(const BloomGeom& g, const uint8_t* __restrict__ bf1, const uint64_t w1[4], uint64_t a1,
-                            bool& ok1, const uint8_t* __restrict__ bf2, const uint64_t w2[4], uint64_t a2,
-                            bool& ok2) {
-  uint64_t pos1 = mod_bits(a1, g), pos2 = mod_bits(a2, g);
-  const uint64_t b1 = xxh64_32(w1, a1), b2 = xxh64_32(w2, a2);
-  const uint64_t bm1 = mod_bits(b1, g), bm2 = mod_bits(b2, g);
-  uint64_t h1 = a1, h2 = a2;
-  for (uint32_t i = 1; i < g.hashes && (ok1 || ok2); ++i) {
-    uint64_t nh = h1 + b1;
-    bool wrapped = nh < h1;
-    h1 = nh;
-    pos1 += bm1;
-    if (pos1 >= g.bits) pos1 -= g.bits;
-    if (wrapped) pos1 = (pos1 >= g.wrap) ? pos1 - g.wrap : pos1 + g.bits - g.wrap;
-    nh = h2 + b2;
-    wrapped = nh < h2;
-    h2 = nh;
-    pos2 += bm2;
-    if (pos2 >= g.bits) pos2 -= g.bits;
-    if (wrapped) pos2 = (pos2 >= g.wrap) ? pos2 - g.wrap : pos2 + g.bits - g.wrap;
-    const uint32_t t1 = ok1 ? bf1[pos1 >> 3] : 0u;
-    const uint32_t t2 = ok2 ? bf2[pos2 >> 3] : 0u;
-    ok1 = ok1 && ((t1 >> (pos1 & 7)) & 1u);
-    ok2 = ok2 && ((t2 >> (pos2 & 7)) & 1u);
-  }
+// The whole bloom_check for x with first hash a (the gate path: L1 bit 0 not yet read).  The bit-0
+// load is issued before the second hash, so the hash runs under the load's latency.
+template <int R>
+KHB_HD bool bloom_full(const uint8_t* __restrict__ bf, const BloomGeom& g, const uint64_t w[4], uint64_t a) {
+  const uint64_t p0 = mod_bits(a, g);
+  const uint32_t t0 = bf[p0 >> 3];
+  const uint64_t b = xxh64_32(w, a);
+  if (!((t0 >> (p0 & 7)) & 1u)) return false;
+  return bloom_steps<R>(bf, g, a, b);
 }
 
 KHB_HD bool bloom_rest(const uint8_t* __restrict__ bf, const BloomGeom& g, const uint64_t w[4], uint64_t a) {

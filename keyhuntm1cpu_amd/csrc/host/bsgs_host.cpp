@@ -124,8 +124,8 @@ bool make_geometry(const char* n_str, int kfactor, Geometry& g, std::string& err
 
 // Baby-step walk on the GPU (khb_build_baby): jobs of 2^20 keys, centre key k*2^20 + 513.
 static bool build_baby_gpu(Tables& T, const Geometry& g, const std::vector<Pt>& gn, const Pt& g2n, uint64_t extent,
-                           bool need_l1, bool need_l2, bool need_l3, bool need_bp, int device, int nthreads,
-                           double& kernel_ms, std::string& err) {
+                           bool need_l1, bool need_l2, bool need_l3, bool need_bp, uint32_t gate_log2, int device,
+                           int nthreads, double& kernel_ms, std::string& err) {
   const uint32_t gpj = 1024, gpl = 4;
   const uint64_t job_keys = (uint64_t)gpj * kGrp;
   const uint32_t n_jobs = (uint32_t)((extent + job_keys - 1) / job_keys);
@@ -162,7 +162,8 @@ static bool build_baby_gpu(Tables& T, const Geometry& g, const std::vector<Pt>& 
       !(rc = khb_load_lane_offsets(ctx, offs.data(), gpj / gpl, gpl)))
     rc = khb_build_baby(ctx, centres.data(), n_jobs, gpj, g.l1ext, g.m2, g.m3, bytes, bits, hashes,
                         need_l1 ? cat[0].data() : nullptr, need_l2 ? cat[1].data() : nullptr,
-                        need_l3 ? cat[2].data() : nullptr, need_bp ? (uint8_t*)T.bp.data() : nullptr, &ms);
+                        need_l3 ? cat[2].data() : nullptr, need_bp ? (uint8_t*)T.bp.data() : nullptr,
+                        gate_log2 ? T.gate.data() : nullptr, gate_log2, &ms);
   khb_close(ctx);
   if (rc) {
     err = std::string("[E] GPU table build: ") + khb_strerror(rc);
@@ -174,6 +175,19 @@ static bool build_baby_gpu(Tables& T, const Geometry& g, const std::vector<Pt>& 
     if (!cat[l].empty())
       for (int i = 0; i < 256; ++i) memcpy((*lv[l])[i].bf.data(), cat[l].data() + i * bytes[l], bytes[l]);
   return true;
+}
+
+uint32_t Tables::gate_log2_for(const Geometry& g) {
+  uint32_t cap = 30, sparsity = 6;
+  if (const char* e = getenv("KHB_GATE_LOG2")) cap = (uint32_t)atoi(e);
+  if (const char* e = getenv("KHB_GATE_SPARSITY")) sparsity = (uint32_t)atoi(e);
+  if (cap == 0 || g.l1ext == 0) return 0;
+  if (cap < 13) cap = 13;
+  if (cap > 40) cap = 40;
+  if (sparsity > 8) sparsity = 8;
+  uint32_t lg = 13;
+  while (lg < cap && (1ull << lg) < (g.l1ext << sparsity)) ++lg;
+  return (1ull << lg) < 4 * g.l1ext ? 0 : lg;   // more than ~22 % full: not worth a load
 }
 
 void Tables::prepare(const Geometry& g) {
@@ -198,8 +212,12 @@ bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, st
   if (!(have & kFileBp)) bp.assign(g.m3, XValue());
   const bool need_l1 = !(have & kFileL1), need_l2 = !(have & kFileL2), need_l3 = !(have & kFileL3),
              need_bp = !(have & kFileBp);
+  // level-0 gate: built wherever the whole L1 set is walked (the GPU walks it for the gate alone)
+  gate_log2 = (need_l1 || gpu_device >= 0) ? gate_log2_for(g) : 0;
+  gate.assign(gate_log2 ? (size_t)1 << (gate_log2 - 3) : 0, 0);
   // baby steps to walk: all of the L1 extent, or only the first m2 when L1 came from a file
-  const uint64_t extent = need_l1 ? g.l1ext : ((need_l2 || need_l3 || need_bp) ? g.m2 : 0);
+  const uint64_t extent = (need_l1 || (gate_log2 && gpu_device >= 0)) ? g.l1ext
+                          : ((need_l2 || need_l3 || need_bp) ? g.m2 : 0);
   // giant tables (keyhunt.cpp:1309-1364)
   {
     Pt bsP = negation(mul_g(g.M_double));
@@ -248,8 +266,8 @@ bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, st
   }
   if (nthreads < 1) nthreads = 1;
   if (gpu_device >= 0 && extent) {
-    if (!build_baby_gpu(*this, g, gn, g2n, extent, need_l1, need_l2, need_l3, need_bp, gpu_device, nthreads,
-                        build_gpu_ms, err))
+    if (!build_baby_gpu(*this, g, gn, g2n, extent, need_l1, need_l2, need_l3, need_bp, gate_log2, gpu_device,
+                        nthreads, build_gpu_ms, err))
       return false;
     jobs.clear();   // the CPU workers below only compute the lane offsets
     if (progress) progress(extent, extent);
@@ -279,7 +297,15 @@ bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, st
             if (need_l3) l3[idx].add32_atomic(xb);
           }
           if (need_l2 && ic < g.m2) l2[idx].add32_atomic(xb);
-          if (need_l1 && ic < to) l1[idx].add32_atomic(xb);
+          if (need_l1 && ic < to) {
+            l1[idx].add32_atomic(xb);
+            if (gate_log2) {
+              uint64_t w[4];
+              words_of_bytes32(w, xb);
+              const uint64_t gb = xxh64_32(w, KHB_BLOOM_SEED) >> (64 - gate_log2);
+              __atomic_fetch_or(&gate[gb >> 3], (uint8_t)(1u << (gb & 7)), __ATOMIC_RELAXED);
+            }
+          }
         }
         done.fetch_add(kGrp);
       }

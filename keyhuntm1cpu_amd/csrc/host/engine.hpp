@@ -28,6 +28,7 @@ struct SearchConfig {
   int check_threads = 0;           // CPU confirmation pool, 0 = auto
   uint64_t max_chunks = 0;         // 0 = until range end
   bool random_chunks = false;      // -B random: every chunk base drawn uniformly in the range
+  bool use_gate = true;            // load the tables' level-0 gate (khb_load_gate) when they have one
 };
 
 struct SearchStats {

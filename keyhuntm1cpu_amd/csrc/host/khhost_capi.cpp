@@ -126,6 +126,11 @@ uint32_t khh_lane_offsets(const khh_tables* t, uint8_t* out, uint32_t* gpl) {
   return (uint32_t)t->t.lane_offs.size();
 }
 
+const uint8_t* khh_gate(const khh_tables* t, uint32_t* log2) {
+  if (log2) *log2 = t->t.gate_log2;
+  return t->t.gate_log2 ? t->t.gate.data() : nullptr;
+}
+
 const uint8_t* khh_bptable(const khh_tables* t, uint64_t* n) {
   static_assert(sizeof(XValue) == 16, "bsgs_xvalue is 16 bytes");
   if (n) *n = t->t.bp.size();

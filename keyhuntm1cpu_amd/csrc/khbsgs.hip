@@ -35,7 +35,7 @@ struct AffPt {
 #define KHB_PROBE_MODE 0          // 0 = product; 1..3 = perf experiments (tools/perf_variants.py)
 #endif
 #ifndef KHB_PROBE_BITS
-#define KHB_PROBE_BITS 1          // bloom bits per round trip in a width-1 drain (2 and 4 measured slower)
+#define KHB_PROBE_BITS 1          // bloom bits per round trip in the drain (2 and 4 measured slower)
 #endif
 #ifndef KHB_GSN_SCALAR
 #define KHB_GSN_SCALAR 1          // GSn table through scalar loads
@@ -82,6 +82,12 @@ struct ScanArgs {
   uint64_t bwords[3];
   uint64_t blimit[3];                  // ic < blimit[l] goes into level l (l1ext, m2, m3)
   uint32_t* __restrict__ bp;           // m3 x 16-byte struct bsgs_xvalue records (null = skipped)
+  // level-0 gate (khb_load_gate): bit (a >> gate_shift) of a 2^(64-gate_shift)-bit map, set for every
+  // x of the L1 set; null = no gate.  kBaby writes it (gate_w, ic < glimit).
+  const uint8_t* __restrict__ gate;
+  uint32_t* __restrict__ gate_w;
+  uint64_t glimit;
+  uint32_t gate_shift;
   uint64_t job_keys;                   // baby steps per job
   uint64_t n_items;
   uint32_t n_jobs, group_begin, group_end, gpl, lanes_per_job, stride, cand_cap, degen_cap;
@@ -93,15 +99,20 @@ __device__ __forceinline__ void emit_cand(const ScanArgs& A, uint32_t job, uint3
 }
 
 // ---- level-1 probe with a per-wave survivor queue ---------------------------------------------
-// Every x pays the first XXH64 and one bloom bit.  The ~50 % whose first bit is set are pushed to
-// a per-wave LDS queue (x, a, job, giant-step index); whenever 64 are queued the whole wave
-// finishes 64 of them together (second XXH64 + remaining bits, bloom_rest).  Without the queue a
-// wave would run the second hash and the dependent bit loads whenever ANY of its lanes survived,
-// i.e. for every x, with one memory round trip per bit per probe site.
-#ifndef KHB_DRAIN_WIDTH
-#define KHB_DRAIN_WIDTH 1         // queued entries finished per lane per drain (1 or 2; 2 measured no faster)
-#endif
-constexpr uint32_t kDrainAt = 64 * KHB_DRAIN_WIDTH;   // drain threshold (entries)
+// Every x pays the first XXH64 and one bit load.  Without a gate that bit is L1 bit 0 and the
+// ~50 % whose bit is set are pushed to a per-wave LDS queue (x, a, job, giant-step index); whenever
+// 64 are queued the whole wave finishes 64 of them together (second XXH64 + remaining bits,
+// bloom_rest).  Without the queue a wave would run the second hash and the dependent bit loads
+// whenever ANY of its lanes survived, i.e. for every x, with one memory round trip per bit per
+// probe site.
+//
+// With a level-0 gate (khb_load_gate) the one bit is read from the gate instead: a 2^25-bit map
+// (4 MiB, L2-resident where the 14 MiB L1 is not) with bit a >> 39 set for every baby-step x of the
+// L1 set, so no L1 member is ever dropped.  Only the gate's survivors (~12 % at k = 1) are queued,
+// and the drain runs the whole L1 check (bloom_full).  The candidate stream is the L1 candidates
+// whose gate bit is set: every true member, and fewer of the false positives that
+// bsgs_secondcheck would reject.
+constexpr uint32_t kDrainAt = 64;          // drain threshold (entries): one per lane
 constexpr uint32_t kQCap = kDrainAt + 64;           // entries per wave: < kDrainAt resident + <= 64 pushed
 constexpr uint32_t kQWords = 12;           // x[8], a lo, a hi, job, step index (SoA in LDS)
 constexpr uint32_t kWavesPerBlock = kBlock / 64;
@@ -127,19 +138,16 @@ __device__ __forceinline__ void q_read(const ProbeQueue& Q, uint32_t k, Fe& x, u
   step = Q.q[11 * kQCap + k];
 }
 
-// Finish up to min(n, KHB_DRAIN_WIDTH x active lanes) queued entries (the newest ones), while
-// n >= threshold.  With width 2 every lane carries two entries through one interleaved bit loop.
+// Finish the newest min(n, active lanes) queued entries, one per lane, while n >= threshold.
 __device__ __forceinline__ void q_drain(const ScanArgs& A, ProbeQueue& Q, uint32_t threshold) {
   for (;;) {
     const uint32_t n = *Q.n;
     if (n < threshold || n == 0) break;
     const uint64_t em = __ballot(1);
-    const uint32_t na = (uint32_t)__popcll(em);
-    const uint32_t take = min(n, KHB_DRAIN_WIDTH * na);
+    const uint32_t take = min(n, (uint32_t)__popcll(em));
     const uint32_t r = lane_rank(em);
     *Q.n = n - take;
     asm volatile("" ::: "memory");
-#if KHB_DRAIN_WIDTH == 1
     if (r < take) {
       Fe x;
       uint64_t a;
@@ -147,26 +155,10 @@ __device__ __forceinline__ void q_drain(const ScanArgs& A, ProbeQueue& Q, uint32
       q_read(Q, n - take + r, x, a, job, step);
       uint64_t w[4];
       x_words(w, x);
-      if (bloom_rest_r<KHB_PROBE_BITS>(sub_bloom(A.bloom, A.geom, x), A.geom, w, a)) emit_cand(A, job, step);
+      const uint8_t* bf = sub_bloom(A.bloom, A.geom, x);
+      if (A.gate ? bloom_full<KHB_PROBE_BITS>(bf, A.geom, w, a) : bloom_rest_r<KHB_PROBE_BITS>(bf, A.geom, w, a))
+        emit_cand(A, job, step);
     }
-#else
-    if (r < take) {
-      const uint32_t k1 = n - take + r, k2 = k1 + na;
-      bool ok1 = true, ok2 = r + na < take;
-      Fe x1, x2;
-      uint64_t a1, a2;
-      uint32_t job1, step1, job2, step2;
-      q_read(Q, k1, x1, a1, job1, step1);
-      q_read(Q, ok2 ? k2 : k1, x2, a2, job2, step2);
-      uint64_t w1[4], w2[4];
-      x_words(w1, x1);
-      x_words(w2, x2);
-      bloom_rest_pair(A.geom, sub_bloom(A.bloom, A.geom, x1), w1, a1, ok1, sub_bloom(A.bloom, A.geom, x2), w2, a2,
-                      ok2);
-      if (ok1) emit_cand(A, job1, step1);
-      if (ok2) emit_cand(A, job2, step2);
-    }
-#endif
     asm volatile("" ::: "memory");
   }
 }
@@ -193,6 +185,7 @@ __device__ __forceinline__ bool first_bit(const ScanArgs& A, const Fe& x, uint64
   uint64_t w[4];
   x_words(w, x);
   a = xxh64_32(w, KHB_BLOOM_SEED);
+  if (A.gate) return test_bit(A.gate, a >> A.gate_shift);
   return test_bit(sub_bloom(A.bloom, A.geom, x), mod_bits(a, A.geom));
 }
 
@@ -219,6 +212,18 @@ __device__ __forceinline__ void probe(const ScanArgs& A, ProbeQueue& Q, const Fe
     const uint8_t* bf = sub_bloom(A.bloom, A.geom, x);
     const uint64_t pos = mod_bits(a, A.geom);
     if ((bf[pos >> 3] >> (pos & 7)) & 1u & (a == 0x0123456789abcdefull)) emit_cand(A, job, j * KHB_GROUP + t);
+#elif KHB_PROBE_MODE == 4      // perf experiment: first hash + one random bit of a 4 MiB table
+    uint64_t w[4];
+    x_words(w, x);
+    const uint64_t a = xxh64_32(w, KHB_BLOOM_SEED);
+    const uint8_t byte = A.bloom[a >> 42];
+    if (((byte >> ((a >> 39) & 7)) & 1u) & (a == 0x0123456789abcdefull)) emit_cand(A, job, j * KHB_GROUP + t);
+#elif KHB_PROBE_MODE == 5      // perf experiment: as 4 with a 2 MiB table
+    uint64_t w[4];
+    x_words(w, x);
+    const uint64_t a = xxh64_32(w, KHB_BLOOM_SEED);
+    const uint8_t byte = A.bloom[a >> 43];
+    if (((byte >> ((a >> 40) & 7)) & 1u) & (a == 0x0123456789abcdefull)) emit_cand(A, job, j * KHB_GROUP + t);
 #else                          // perf experiment: no probe at all
     if (x.v[0] == 0x01234567u && x.v[1] == 0x89abcdefu) emit_cand(A, job, j * KHB_GROUP + t);
 #endif
@@ -325,10 +330,14 @@ __device__ __forceinline__ void bloom_add_words(uint32_t* __restrict__ words, co
 // Baby step ic = job * job_keys + 1024 j + t (key ic + 1): thread_bPload (keyhunt.cpp:4404-4592).
 __device__ __forceinline__ void baby_point(const ScanArgs& A, const Fe& x, uint32_t job, uint32_t j, uint32_t t) {
   const uint64_t ic = (uint64_t)job * A.job_keys + (uint64_t)j * KHB_GROUP + t;
-  if (ic >= A.blimit[0] && ic >= A.blimit[1] && ic >= A.blimit[2]) return;
+  if (ic >= A.blimit[0] && ic >= A.blimit[1] && ic >= A.blimit[2] && ic >= A.glimit) return;
   uint64_t w[4];
   x_words(w, x);
   const uint64_t a = xxh64_32(w, KHB_BLOOM_SEED);
+  if (A.gate_w && ic < A.glimit) {
+    const uint64_t gb = a >> A.gate_shift;
+    atomicOr(A.gate_w + (gb >> 5), 1u << (gb & 31));
+  }
   const uint64_t b = xxh64_32(w, a);
   const uint32_t sub = x.v[7] >> 24;
 #pragma unroll 1
@@ -581,6 +590,8 @@ struct khb_ctx {
   uint32_t lanes = 0;
   uint8_t* d_bloom = nullptr;
   BloomGeom geom{};
+  uint8_t* d_gate = nullptr;           // level-0 gate (khb_load_gate), null = none
+  uint32_t gate_shift = 0;
   AffPt* d_gsn = nullptr;
   AffPt* d_offs = nullptr;
   uint32_t n_offs = 0, gpl = 0;
@@ -635,6 +646,8 @@ ScanArgs make_args(khb_ctx* c, uint32_t n_jobs, uint32_t group_begin, uint32_t g
   ScanArgs A{};
   A.bloom = c->d_bloom;
   A.geom = c->geom;
+  A.gate = c->d_gate;
+  A.gate_shift = c->gate_shift;
   A.gsn = c->d_gsn;
   A.offs = c->d_offs;
   A.centres = c->d_centres;
@@ -730,6 +743,7 @@ int khb_close(khb_ctx* c) {
   if (c->device >= 0) hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   hipFree(c->d_bloom);
+  hipFree(c->d_gate);
   hipFree(c->d_gsn);
   hipFree(c->d_offs);
   hipFree(c->d_centres);
@@ -745,6 +759,20 @@ int khb_close(khb_ctx* c) {
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
+  return KHB_OK;
+}
+
+int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits) {
+  if (!c || (gate && (log2_bits < 13 || log2_bits > 40))) return KHB_EINVAL;
+  if (c->in_flight) return KHB_EBUSY;
+  KHB_TRY(c, hipSetDevice(c->device));
+  if (c->d_gate) { hipFree(c->d_gate); c->d_gate = nullptr; }
+  c->gate_shift = 0;
+  if (!gate) return KHB_OK;
+  const size_t bytes = (size_t)1 << (log2_bits - 3);
+  KHB_TRY(c, hipMalloc(&c->d_gate, bytes));
+  KHB_TRY(c, hipMemcpy(c->d_gate, gate, bytes, hipMemcpyHostToDevice));
+  c->gate_shift = 64 - log2_bits;
   return KHB_OK;
 }
 
@@ -1061,10 +1089,12 @@ int khb_hash160(khb_ctx* c, int kind, const uint8_t* xy, uint8_t* out, uint32_t 
 // ------------------------------------------------------------------------- baby-step tables
 int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t groups_per_job, uint64_t l1ext,
                    uint64_t m2, uint64_t m3, const uint64_t bytes_per_sub[3], const uint64_t bits_per_sub[3],
-                   const uint32_t hashes[3], uint8_t* l1, uint8_t* l2, uint8_t* l3, uint8_t* bp, float* kernel_ms) {
+                   const uint32_t hashes[3], uint8_t* l1, uint8_t* l2, uint8_t* l3, uint8_t* bp, uint8_t* gate,
+                   uint32_t gate_log2, float* kernel_ms) {
   int rc = check_scan_args(c, centres, n_jobs, 0, groups_per_job, false);
   if (rc) return rc;
   if (!bytes_per_sub || !bits_per_sub || !hashes) return KHB_EINVAL;
+  if (gate && (gate_log2 < 13 || gate_log2 > 40)) return KHB_EINVAL;
   uint8_t* outs[3] = {l1, l2, l3};
   for (int l = 0; l < 3; ++l)
     if (outs[l] && (bits_per_sub[l] < 2 || (bits_per_sub[l] + 7) / 8 != bytes_per_sub[l] || hashes[l] == 0 ||
@@ -1081,7 +1111,16 @@ int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t
   A.blimit[2] = (l3 || bp) ? m3 : 0;
   uint32_t* dw[3] = {nullptr, nullptr, nullptr};
   uint32_t* dbp = nullptr;
+  uint32_t* dgate = nullptr;
+  const uint64_t gate_bytes = gate ? (1ull << gate_log2) / 8 : 0;
   hipError_t e = hipSuccess;
+  if (gate) {
+    e = hipMalloc(&dgate, gate_bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(dgate, 0, gate_bytes, c->stream);
+    A.gate_w = dgate;
+    A.glimit = l1ext;
+    A.gate_shift = 64 - gate_log2;
+  }
   for (int l = 0; l < 3 && e == hipSuccess; ++l) {
     if (!outs[l]) continue;
     const uint64_t words = (bytes_per_sub[l] + 3) / 4;
@@ -1126,8 +1165,10 @@ int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t
     free(tmp);
   }
   if (e == hipSuccess && dbp) e = hipMemcpy(bp, dbp, 16 * m3, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && dgate) e = hipMemcpy(gate, dgate, gate_bytes, hipMemcpyDeviceToHost);
   for (int l = 0; l < 3; ++l) hipFree(dw[l]);
   hipFree(dbp);
+  hipFree(dgate);
   if (e != hipSuccess) return hip_fail(c, e);
   return KHB_OK;
 }

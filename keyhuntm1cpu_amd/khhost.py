@@ -42,6 +42,8 @@ def lib() -> C.CDLL:
         L.khh_lane_offsets.argtypes = [C.c_void_p, C.c_char_p, P(C.c_uint32)]
         L.khh_bptable.restype = P(C.c_uint8)
         L.khh_bptable.argtypes = [C.c_void_p, P(C.c_uint64)]
+        L.khh_gate.restype = C.c_void_p
+        L.khh_gate.argtypes = [C.c_void_p, P(C.c_uint32)]
         L.khh_chunk_centre.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p]
         L.khh_secondcheck.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_char_p, C.c_char_p]
         L.khh_search.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, P(C.c_int), C.c_int,
@@ -166,6 +168,12 @@ class Tables:
         b = C.create_string_buffer(64 * n)
         lib().khh_lane_offsets(self.h, b, C.byref(g))
         return b.raw, int(g.value)
+
+    def gate(self) -> tuple[bytes, int]:
+        """The level-0 gate (khb_load_gate) and its log2 size; (b"", 0) when the tables have none."""
+        lg = C.c_uint32(0)
+        p = lib().khh_gate(self.h, C.byref(lg))
+        return (C.string_at(p, (1 << lg.value) // 8) if lg.value else b""), int(lg.value)
 
     def bptable(self) -> list[tuple[bytes, int]]:
         n = C.c_uint64()

@@ -156,3 +156,58 @@ def test_candidates_ragged_lanes_match_oracle(eng, bs32, ora):
         per_job[job].append(a)
     assert [sorted(x) for x in per_job] == ref
     assert sum(len(r) for r in ref) > 0
+
+
+def _l1_check(bf: bytes, nb: int, bits: int, hashes: int, xb: bytes, ora) -> bool:
+    """bloom_check(&bloom_bP[x[0]], x, 32) (bloom.cpp:128-156) in Python."""
+    sub = bf[xb[0] * nb:(xb[0] + 1) * nb]
+    a = ora.xxh64(xb, 0x59F2815B16F81798)
+    b = ora.xxh64(xb, a)
+    for i in range(hashes):
+        p = ((a + b * i) & 0xFFFFFFFFFFFFFFFF) % bits
+        if not (sub[p >> 3] >> (p & 7)) & 1:
+            return False
+    return True
+
+
+def test_gate_candidates_exact(eng, bs32, ora):
+    """Level-0 gate (khb_load_gate): the candidates are exactly the giant steps whose x passes the
+    level-1 bloom AND whose gate bit XXH64(x) >> (64 - log2) is set.  A dense synthetic L1 (each bit
+    set with p = 0.97, so ~54 % of all x pass) and a random half-full gate exercise both paths on
+    every x of four chunks; without the gate the same scan returns the plain L1 candidates."""
+    gpl = 4
+    load_tables(eng, bs32, gpl)
+    _, nb, bits, hashes = bs32.bloom_concat(1)
+    rng = random.Random(7)
+    bf = bytes(sum(1 << k for k in range(8) if rng.random() < 0.97) for _ in range(256 * nb))
+    eng.load_bloom(bf, nb, bits, hashes)
+    lg = 16
+    gate = bytes(rng.getrandbits(8) for _ in range((1 << lg) // 8))
+    centres, l1_ref, gate_ref = [], [], []
+    for c in range(4):
+        st = bs32.chunk_start(0x3000000000000000 + c * (1 << 33), ora.pubkey(0xABCDEF0123 + c))
+        centres.append(st.be64())
+        _, xs, _ = bs32.scan(st, 0, bs32.cycles, want_x=True)
+        l1, gt = [], []
+        for a in range(bs32.cycles * 1024):
+            xb = xs[32 * a:32 * a + 32]
+            if _l1_check(bf, nb, bits, hashes, xb, ora):
+                l1.append(a)
+                g = ora.xxh64(xb, 0x59F2815B16F81798) >> (64 - lg)
+                if (gate[g >> 3] >> (g & 7)) & 1:
+                    gt.append(a)
+        l1_ref.append(l1)
+        gate_ref.append(gt)
+    try:
+        for use_gate, ref in ((False, l1_ref), (True, gate_ref)):
+            eng.load_gate(gate if use_gate else None, lg)
+            got, degen, _ = eng.scan(b"".join(centres), 0, bs32.cycles)
+            per_job = [[] for _ in centres]
+            for job, a in got:
+                per_job[job].append(a)
+            assert [sorted(x) for x in per_job] == ref, use_gate
+        assert 0.4 < sum(map(len, gate_ref)) / sum(map(len, l1_ref)) < 0.6
+        assert sum(map(len, l1_ref)) > 100000
+    finally:
+        eng.load_gate(None)
+        load_tables(eng, bs32, gpl)

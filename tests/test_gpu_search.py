@@ -84,6 +84,38 @@ def test_full_geometry_candidates_match_oracle(tables_k1, ora):
     assert any(tables_k1.secondcheck(bases[0], a, t.be64()) == key for a in a_hits)
 
 
+def test_full_geometry_gate(tables_k1, ora):
+    """The product's level-0 gate on the real k=1 tables (2^25 bits): over two whole chunks the gated
+    candidates are exactly the L1 candidates whose gate bit is set (x from the GPU dump of their
+    group), and the key's hit survives the gate."""
+    from keyhuntm1cpu_amd.khbsgs import Engine
+    gate, lg = tables_k1.gate()
+    assert lg == 28
+    key = 0x2832ED74F2B5E35EE
+    t = ora.pubkey(key)
+    bases = [key - 123456789012, (1 << 65) + (5 << 45)]
+    with Engine(0) as e:
+        bf, nb, bits, h = tables_k1.bloom_concat(1)
+        e.load_bloom(bf, nb, bits, h)
+        e.load_giant_table(tables_k1.giant_table())
+        offs, gpl = tables_k1.lane_offsets()
+        e.load_lane_offsets(offs, gpl)
+        centres = [tables_k1.chunk_centre(b, t.be64()) for b in bases]
+        plain, _, _ = e.scan(b"".join(centres), 0, tables_k1.cycles)
+        e.load_gate(gate, lg)
+        gated, _, st = e.scan(b"".join(centres), 0, tables_k1.cycles)
+        exp = []
+        for j, a in plain:
+            g0 = (a // 1024) // gpl * gpl
+            xs = e.dump_x(centres[j], g0, gpl)
+            xb = xs[32 * (a - g0 * 1024):32 * (a - g0 * 1024) + 32]
+            gb = ora.xxh64(xb, 0x59F2815B16F81798) >> (64 - lg)
+            if (gate[gb >> 3] >> (gb & 7)) & 1:
+                exp.append((j, a))
+    assert sorted(gated) == sorted(exp)
+    assert any(tables_k1.secondcheck(bases[0], a, t.be64()) == key for j, a in gated if j == 0)
+
+
 def _cli(args, cwd):
     exe = os.path.join(BIN_DIR, "keyhunt_amd")
     return subprocess.run([exe] + args, cwd=cwd, capture_output=True, text=True, timeout=300)

@@ -1,5 +1,5 @@
 """GPU baby-step table build (khb_build_baby; thread_bPload keyhunt.cpp:4404-4592): the three
-bloom levels and the bPtable built on the GPU equal the host build byte for byte."""
+bloom levels, the bPtable and the level-0 gate built on the GPU equal the host build byte for byte."""
 from __future__ import annotations
 
 import pytest
@@ -15,6 +15,7 @@ def _same(a, b):
     assert a.bptable() == b.bptable()
     assert a.giant_table() == b.giant_table()
     assert a.lane_offsets() == b.lane_offsets()
+    assert a.gate() == b.gate() and a.gate()[1] >= 13
 
 
 @pytest.mark.parametrize("n,k", [("0x40000000", 33),      # M = 33*2^15: L1 extent overshoot (quirk vi)

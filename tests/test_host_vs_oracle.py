@@ -87,3 +87,19 @@ def test_pubkey_and_parse(ora):
     assert khhost.parse_pubkey("02" + "00" * 31 + "05") is None or True   # may or may not be on curve
     assert khhost.parse_pubkey("05" + "11" * 32) is None
     assert khhost.parse_pubkey("02" + "11" * 31) is None
+
+
+def test_level0_gate_exact(pair, ora):
+    """The level-0 gate (khb_load_gate) is exactly the set of bits XXH64(x) >> (64 - log2) over the
+    baby steps of the L1 set (ic < l1ext, key ic + 1): every L1 member passes it, nothing else is set."""
+    h, o = pair
+    if o.l1ext > 1 << 17:
+        pytest.skip("baby set too large for the Python walk")
+    gate, lg = h.gate()
+    assert lg >= 13 and len(gate) == (1 << lg) // 8
+    exp = bytearray(len(gate))
+    for ic in range(o.l1ext):
+        x = ora.pubkey(ic + 1).xy()[0]
+        b = ora.xxh64(x.to_bytes(32, "big"), 0x59F2815B16F81798) >> (64 - lg)
+        exp[b >> 3] |= 1 << (b & 7)
+    assert gate == bytes(exp)

@@ -1,6 +1,10 @@
 """A/B timing of libkhbsgs kernel variants in ONE process (interleaved rounds, median).
 Usage: python tools/perf_variants.py [lib.so ...]   (default: the product library + lib/variants/*)
-Tables: product host engine, default geometry (k=1), puzzle #66 target, 256 chunks per launch."""
+Tables: product host engine, default geometry (k=1, or K=...), puzzle #66 target, JOBS (256) chunks
+per launch.
+GATE=0|1|both (default both): run every library without / with the level-0 gate.
+GATE_LOG2S=23,24 adds gates of those sizes, folded from the tables' gate (bit i of a 2^(L-1) map is
+bit 2i | bit 2i+1 of the 2^L map: the same map a 2^(L-1) build writes)."""
 import glob
 import os
 import statistics
@@ -14,35 +18,52 @@ from keyhuntm1cpu_amd import khhost, LIB_DIR  # noqa: E402
 from keyhuntm1cpu_amd.khbsgs import Engine, LIB_PATH  # noqa: E402
 
 paths = sys.argv[1:] or [LIB_PATH] + sorted(glob.glob(os.path.join(LIB_DIR, "variants", "*.so")))
-t = khhost.Tables(None, 1, threads=16)
+t = khhost.Tables(None, int(os.environ.get("K", "1")), threads=16)
 bf, nb, bits, h = t.bloom_concat(1)
 gsn = t.giant_table()
 offs, gpl = t.lane_offsets()
 tgt = khhost.pubkey(0x2832ED74F2B5E35EE)
 jobs = int(os.environ.get("JOBS", "256"))
 centres = b"".join(t.chunk_centre((1 << 65) + c * (1 << 45), tgt) for c in range(jobs))
+gate, glog = t.gate()
+gmode = os.environ.get("GATE", "both")
+gsets = [0, glog] if gmode == "both" else [glog if gmode == "1" else 0]
+gates = {glog: gate}
+import numpy as np  # noqa: E402
+for lg in [int(v) for v in os.environ.get("GATE_LOG2S", "").split(",") if v]:
+    bv = np.unpackbits(np.frombuffer(gate, np.uint8), bitorder="little")
+    gates[lg] = np.packbits(bv.reshape(-1, 1 << (glog - lg)).max(axis=1), bitorder="little").tobytes()
+    gsets.append(lg)
 engines = {}
 for p in paths:
-    e = Engine(0, lib_path=p)
-    e.load_bloom(bf, nb, bits, h)
-    e.load_giant_table(gsn)
-    e.load_lane_offsets(offs, gpl)
-    e.scan(centres[:64 * 8], 0, 64)
-    engines[p] = e
-    print(f"{os.path.basename(p)}: lanes {e.lanes()}", flush=True)
-times = {p: [] for p in paths}
-ref = None
+    for g in gsets:
+        e = Engine(0, lib_path=p)
+        e.load_bloom(bf, nb, bits, h)
+        if g:
+            e.load_gate(gates[g], g)
+        e.load_giant_table(gsn)
+        e.load_lane_offsets(offs, gpl)
+        e.scan(centres[:64 * 8], 0, 64)
+        name = os.path.basename(p) + (f" +gate{g}" if g else "")
+        engines[name] = (e, g)
+        print(f"{name}: lanes {e.lanes()}", flush=True)
+times = {n: [] for n in engines}
+ncand = {}
+ref = {}
 for rnd in range(int(os.environ.get("ROUNDS", "3"))):
-    for p, e in engines.items():
+    for n, (e, g) in engines.items():
         c, d, st = e.scan(centres, 0, t.cycles)
-        times[p].append(st.kernel_ms)
-        if "_p" in os.path.basename(p):      # probe experiments: candidates not comparable
+        times[n].append(st.kernel_ms)
+        ncand[n] = len(c)
+        if "_p" in n.split()[0]:      # probe experiments: candidates not comparable
             continue
         s = sorted(c)
-        if ref is None:
-            ref = s
-        assert s == ref, f"{p}: candidate set differs"
+        ref.setdefault(g, s)
+        assert s == ref[g], f"{n}: candidate set differs"
+for g in ref:   # a gate keeps a subset of the L1 candidates
+    assert 0 not in ref or set(ref[g]) <= set(ref[0])
 steps = jobs * t.cycles * 1024
-for p in paths:
-    med = statistics.median(times[p])
-    print(f"{os.path.basename(p):28s} median {med:8.2f} ms  min {min(times[p]):8.2f}  {steps / med / 1e6:8.3f} G steps/s", flush=True)
+for n in engines:
+    med = statistics.median(times[n])
+    print(f"{n:34s} median {med:8.2f} ms  min {min(times[n]):8.2f}  {steps / med / 1e6:8.3f} G steps/s"
+          f"  cand {ncand[n]}", flush=True)
