@@ -3,10 +3,14 @@
 
 One step = one GPU scan batch of the product search (libkhhost -> libkhbsgs): host centres for
 256 chunks, the HIP giant-step kernel over all 4096 groups of each chunk (256 x 4096 x 1024 =
-2^30 giant steps), and the CPU confirmation of every level-1 candidate, pipelined exactly as the
-keyhunt_amd CLI runs it.  Tables are built and resident in HBM before
-the timed region.  Multi-GPU: one process per GPU (torch.distributed.run), the -b 66 chunk range
-statically partitioned across ranks (weak scaling; no data-path collective: gloo only times it).
+2^30 giant steps; at k=4, 1024 chunks x 1024 groups), and the CPU confirmation of every level-1
+candidate, pipelined exactly as the keyhunt_amd CLI runs it.  Tables are built and resident in HBM
+before the timed region.  Chunks are sequential 2N-key chunks of -b 66 starting right after the
+chunk holding puzzle #66's (public) key, so the search never stops early on the find and every
+rank times exactly K steps.  Multi-GPU: one process per GPU (torch.distributed.run), rank r owns
+the r-th block of (W + K) x chunks consecutive chunks (weak scaling; no data-path collective:
+gloo only times it).  At N x K x chunks beyond -b 66's 2^20 chunks the blocks run on past 2^66;
+the work per giant step does not depend on the keys.
 
 Prints ONE JSON line (rank 0).  See DESIGN.md §Measurement for the roofline definitions.
 """
@@ -61,7 +65,9 @@ def main():
     # default: >= 30 s of steady state — 700 steps x 2^30 giant steps at ~44 ms
     ap.add_argument("--steps", type=int, default=700)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--chunks", type=int, default=256, help="chunks (2N keys each) per step")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="chunks (2N keys each) per step; default: 2^30 giant steps per step (256 at k=1, "
+                         "1024 at k=4), enough work items to fill every lane")
     ap.add_argument("--k", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -83,10 +89,14 @@ def main():
     t0 = time.time()
     tables = khhost.Tables(None, args.k, threads=host_threads, gpl=4)
     t_build = time.time() - t0
+    if not args.chunks:
+        args.chunks = max(1, (1 << 30) // (tables.cycles * 1024))
     target = puzzle66_target()
     two_n = 2 * (tables.n_low)                     # 2N keys per chunk
-    lo, hi = 1 << 65, 1 << 66                      # -b 66
-    start, end = rank_range(lo, hi, two_n, rank, world)
+    key_chunk = (PUZZLE66_KEY - (1 << 65)) // two_n
+    lo = (1 << 65) + (key_chunk + 1) * two_n      # -b 66, after the key's chunk
+    per_rank = (args.warmup + args.steps) * args.chunks
+    start, end = rank_range(lo, lo + world * per_rank * two_n, two_n, rank, world)
     sess = khhost.Session(tables, devices=[local], chunks_per_batch=args.chunks, check_threads=host_threads)
 
     def sync():
@@ -123,6 +133,9 @@ def main():
         return
     gsps = tot_steps / tmax
     per_launch_steps = args.chunks * tables.cycles * 1024
+    if tot_steps != world * args.steps * per_launch_steps:
+        print(f"[bench] WARNING: timed {tot_steps} giant steps, expected {world * args.steps * per_launch_steps}",
+              file=sys.stderr, flush=True)
     achieved = OPS_PER_STEP * per_launch_steps / (kernel_ms * 1e-3) / 1e12
     roofline = {"bound": "valu", "unit": "Tops/s", "achieved": round(achieved, 3), "peak": PEAK_MULOPS_T,
                 "frac": round(achieved / PEAK_MULOPS_T, 4), "traffic": None,
@@ -158,7 +171,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "real puzzle #66 pubkey (solved key, hash160 == tests/66.rmd), -b 66 range, sequential chunks",
+        "data": "real puzzle #66 pubkey (solved key, hash160 == tests/66.rmd), -b 66 range, sequential "
+                "chunks from the chunk after the key's",
         "config": {"workload": "puzzle66 -m bsgs -b 66 -k %d (BASELINE configs[%s])"
                                % (args.k, {1: "1", 4: "2"}.get(args.k, "1, k varied")),
                    "n": hex(tables.n_low), "bsgs_m": tables.m, "groups_per_chunk": tables.cycles,
