@@ -80,11 +80,11 @@ uint32_t khb_lanes(const khb_ctx* ctx);
 int khb_load_bloom(khb_ctx* ctx, const uint8_t* bf_concat, uint64_t bytes_per_sub, uint64_t bits_per_sub,
                    uint32_t hashes);
 /* Level-0 gate in front of the level-1 probe (no reference counterpart; a superset filter): a map of
- * 2^log2_bits bits, bit (XXH64(x, seed) >> (64 - log2_bits)) set for every baby-step x of the level-1
- * set (bit i of byte i/8, LSB first; khb_build_baby writes one).  With a gate, the giant-step probe
- * reads the gate bit first and runs the level-1 check only when it is set: every level-1 candidate
- * whose gate bit is set is still reported, so no baby-step hit is lost.  gate NULL removes it;
- * log2_bits in [13, 40]. */
+ * 2^log2_bits bits, bit (x mod 2^log2_bits) set for every baby-step x of the level-1 set (x the
+ * canonical x-coordinate as an integer; bit i of byte i/8, LSB first; khb_build_baby writes one).
+ * With a gate, the giant-step probe reads the gate bit first and runs the level-1 check (both
+ * XXH64, all bits) only when it is set: every level-1 candidate whose gate bit is set is still
+ * reported, so no baby-step hit is lost.  gate NULL removes it; log2_bits in [13, 32]. */
 int khb_load_gate(khb_ctx* ctx, const uint8_t* gate, uint32_t log2_bits);
 /* GSn[0..511] and _2GSn (keyhunt.cpp:1325-1338), 513 affine points x||y BE. */
 int khb_load_giant_table(khb_ctx* ctx, const uint8_t* gsn_xy_be);

@@ -183,7 +183,7 @@ uint32_t Tables::gate_log2_for(const Geometry& g) {
   if (const char* e = getenv("KHB_GATE_SPARSITY")) sparsity = (uint32_t)atoi(e);
   if (cap == 0 || g.l1ext == 0) return 0;
   if (cap < 13) cap = 13;
-  if (cap > 40) cap = 40;
+  if (cap > 32) cap = 32;
   if (sparsity > 8) sparsity = 8;
   uint32_t lg = 13;
   while (lg < cap && (1ull << lg) < (g.l1ext << sparsity)) ++lg;
@@ -299,10 +299,9 @@ bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, st
           if (need_l2 && ic < g.m2) l2[idx].add32_atomic(xb);
           if (need_l1 && ic < to) {
             l1[idx].add32_atomic(xb);
-            if (gate_log2) {
-              uint64_t w[4];
-              words_of_bytes32(w, xb);
-              const uint64_t gb = xxh64_32(w, KHB_BLOOM_SEED) >> (64 - gate_log2);
+            if (gate_log2) {   // bit x mod 2^gate_log2 (the low word of x: big-endian bytes 28..31)
+              const uint32_t lo = ((uint32_t)xb[28] << 24) | ((uint32_t)xb[29] << 16) | ((uint32_t)xb[30] << 8) | xb[31];
+              const uint32_t gb = lo & (uint32_t)((1ull << gate_log2) - 1);
               __atomic_fetch_or(&gate[gb >> 3], (uint8_t)(1u << (gb & 7)), __ATOMIC_RELAXED);
             }
           }

@@ -45,7 +45,7 @@ struct Tables {
   std::vector<XValue> bp;                // sorted by value (bsgs_sort)
   Pt gsn[512], g2sn, amp2[32], amp3[32];
   uint32_t gpl = 0;                      // GPU groups per lane
-  // Level-0 gate for the GPU probe (khb_load_gate): bit XXH64(x) >> (64 - gate_log2) set for every
+  // Level-0 gate for the GPU probe (khb_load_gate): bit x mod 2^gate_log2 set for every
   // x of the L1 set.  Built with the baby steps when the L1 set is walked (always on the GPU path;
   // on the CPU path only when L1 is built, not read from a file); gate_log2 = 0: none.
   std::vector<uint8_t> gate;

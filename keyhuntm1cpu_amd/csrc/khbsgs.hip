@@ -82,12 +82,12 @@ struct ScanArgs {
   uint64_t bwords[3];
   uint64_t blimit[3];                  // ic < blimit[l] goes into level l (l1ext, m2, m3)
   uint32_t* __restrict__ bp;           // m3 x 16-byte struct bsgs_xvalue records (null = skipped)
-  // level-0 gate (khb_load_gate): bit (a >> gate_shift) of a 2^(64-gate_shift)-bit map, set for every
+  // level-0 gate (khb_load_gate): bit (x & gate_mask) of a (gate_mask + 1)-bit map, set for every
   // x of the L1 set; null = no gate.  kBaby writes it (gate_w, ic < glimit).
   const uint8_t* __restrict__ gate;
   uint32_t* __restrict__ gate_w;
   uint64_t glimit;
-  uint32_t gate_shift;
+  uint32_t gate_mask;
   uint64_t job_keys;                   // baby steps per job
   uint64_t n_items;
   uint32_t n_jobs, group_begin, group_end, gpl, lanes_per_job, stride, cand_cap, degen_cap;
@@ -99,18 +99,17 @@ __device__ __forceinline__ void emit_cand(const ScanArgs& A, uint32_t job, uint3
 }
 
 // ---- level-1 probe with a per-wave survivor queue ---------------------------------------------
-// Every x pays the first XXH64 and one bit load.  Without a gate that bit is L1 bit 0 and the
-// ~50 % whose bit is set are pushed to a per-wave LDS queue (x, a, job, giant-step index); whenever
-// 64 are queued the whole wave finishes 64 of them together (second XXH64 + remaining bits,
-// bloom_rest).  Without the queue a wave would run the second hash and the dependent bit loads
-// whenever ANY of its lanes survived, i.e. for every x, with one memory round trip per bit per
-// probe site.
+// Without a gate every x pays the first XXH64 and one bit load: L1 bit 0; the ~50 % whose bit is
+// set are pushed to a per-wave LDS queue (x, a, job, giant-step index); whenever 64 are queued the
+// whole wave finishes 64 of them together (second XXH64 + remaining bits, bloom_rest).  Without
+// the queue a wave would run the second hash and the dependent bit loads whenever ANY of its lanes
+// survived, i.e. for every x, with one memory round trip per bit per probe site.
 //
-// With a level-0 gate (khb_load_gate) the one bit is read from the gate instead: a 2^25-bit map
-// (4 MiB, L2-resident where the 14 MiB L1 is not) with bit a >> 39 set for every baby-step x of the
-// L1 set, so no L1 member is ever dropped.  Only the gate's survivors (~12 % at k = 1) are queued,
-// and the drain runs the whole L1 check (bloom_full).  The candidate stream is the L1 candidates
-// whose gate bit is set: every true member, and fewer of the false positives that
+// With a level-0 gate (khb_load_gate) x pays no hash at all: one byte of a 2^L-bit map (L = 28 at
+// k = 1, 32 MiB) addressed by the low L bits of x, with the bit of every baby-step x of the L1 set
+// set, so no L1 member is ever dropped.  Only the gate's survivors (~1.5 %) are queued, and the
+// drain runs the whole L1 check (XXH64 a, bloom_full).  The candidate stream is the L1 candidates
+// whose gate bit is set: every true member, and ~1.5 % of the false positives that
 // bsgs_secondcheck would reject.
 constexpr uint32_t kDrainAt = 64;          // drain threshold (entries): one per lane
 constexpr uint32_t kQCap = kDrainAt + 64;           // entries per wave: < kDrainAt resident + <= 64 pushed
@@ -153,10 +152,12 @@ __device__ __forceinline__ void q_drain(const ScanArgs& A, ProbeQueue& Q, uint32
       uint64_t a;
       uint32_t job, step;
       q_read(Q, n - take + r, x, a, job, step);
+      if (A.gate) fm_canon(x, x);       // gated pushes hold lazy x (scan_group's x_out)
       uint64_t w[4];
       x_words(w, x);
       const uint8_t* bf = sub_bloom(A.bloom, A.geom, x);
-      if (A.gate ? bloom_full<KHB_PROBE_BITS>(bf, A.geom, w, a) : bloom_rest_r<KHB_PROBE_BITS>(bf, A.geom, w, a))
+      if (A.gate ? bloom_full<KHB_PROBE_BITS>(bf, A.geom, w, xxh64_32(w, KHB_BLOOM_SEED))
+                 : bloom_rest_r<KHB_PROBE_BITS>(bf, A.geom, w, a))
         emit_cand(A, job, step);
     }
     asm volatile("" ::: "memory");
@@ -181,11 +182,15 @@ __device__ __forceinline__ void q_push(ProbeQueue& Q, bool hit, const Fe& x, uin
   *Q.n = n + (uint32_t)__popcll(m);
 }
 
+// Gate bit (x & gate_mask), or without a gate L1 bit 0 (a = the first XXH64, queued with x).
 __device__ __forceinline__ bool first_bit(const ScanArgs& A, const Fe& x, uint64_t& a) {
+  if (A.gate) {
+    a = 0;
+    return test_bit(A.gate, x.v[0] & A.gate_mask);
+  }
   uint64_t w[4];
   x_words(w, x);
   a = xxh64_32(w, KHB_BLOOM_SEED);
-  if (A.gate) return test_bit(A.gate, a >> A.gate_shift);
   return test_bit(sub_bloom(A.bloom, A.geom, x), mod_bits(a, A.geom));
 }
 
@@ -335,7 +340,7 @@ __device__ __forceinline__ void baby_point(const ScanArgs& A, const Fe& x, uint3
   x_words(w, x);
   const uint64_t a = xxh64_32(w, KHB_BLOOM_SEED);
   if (A.gate_w && ic < A.glimit) {
-    const uint64_t gb = a >> A.gate_shift;
+    const uint32_t gb = x.v[0] & A.gate_mask;
     atomicOr(A.gate_w + (gb >> 5), 1u << (gb & 31));
   }
   const uint64_t b = xxh64_32(w, a);
@@ -350,6 +355,19 @@ __device__ __forceinline__ void baby_point(const ScanArgs& A, const Fe& x, uint3
     o[1] = (x.v[2] >> 24) | (((x.v[2] >> 16) & 0xffu) << 8);
     o[2] = (uint32_t)ic;
     o[3] = (uint32_t)(ic >> 32);
+  }
+}
+
+// x for the probe.  With a gate only the low word of x is read before the drain, and a lazy x
+// (< 2^256, congruent) differs from the canonical one only when x >= p, which needs x.v[7] ==
+// 0xffffffff (p's top word): the full canonicalisation runs only then (wave-uniform skip, ~2^-26
+// per wave), and the drain canonicalises its survivors before hashing.
+template <int MODE>
+__device__ __forceinline__ void x_out(const ScanArgs& A, Fe& x) {
+  if (MODE == kScan && A.gate) {
+    if (x.v[7] == 0xffffffffu) fm_canon(x, x);
+  } else {
+    fm_canon(x, x);
   }
 }
 
@@ -421,7 +439,7 @@ __device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, Aff
     fm_mul(s, s, idx);
     fm_sqr(x1, s);
     fm_sub(x1, x1, u);
-    fm_canon(x1, x1);
+    x_out<MODE>(A, x1);
     if constexpr (needs_y(MODE)) {
       Fe t;
       fm_sub(t, x1, g.x);
@@ -436,7 +454,7 @@ __device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, Aff
       fm_mul(s, s, idx);
       fm_sqr(x2, s);
       fm_sub(x2, x2, u);
-      fm_canon(x2, x2);
+      x_out<MODE>(A, x2);
       if constexpr (MODE == kBaby) {
         baby_point(A, x1, job, j, kHalf - 1 - (uint32_t)i);
         baby_point(A, x2, job, j, kHalf + 1 + (uint32_t)i);
@@ -591,7 +609,7 @@ struct khb_ctx {
   uint8_t* d_bloom = nullptr;
   BloomGeom geom{};
   uint8_t* d_gate = nullptr;           // level-0 gate (khb_load_gate), null = none
-  uint32_t gate_shift = 0;
+  uint32_t gate_mask = 0;
   AffPt* d_gsn = nullptr;
   AffPt* d_offs = nullptr;
   uint32_t n_offs = 0, gpl = 0;
@@ -647,7 +665,7 @@ ScanArgs make_args(khb_ctx* c, uint32_t n_jobs, uint32_t group_begin, uint32_t g
   A.bloom = c->d_bloom;
   A.geom = c->geom;
   A.gate = c->d_gate;
-  A.gate_shift = c->gate_shift;
+  A.gate_mask = c->gate_mask;
   A.gsn = c->d_gsn;
   A.offs = c->d_offs;
   A.centres = c->d_centres;
@@ -763,16 +781,16 @@ int khb_close(khb_ctx* c) {
 }
 
 int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits) {
-  if (!c || (gate && (log2_bits < 13 || log2_bits > 40))) return KHB_EINVAL;
+  if (!c || (gate && (log2_bits < 13 || log2_bits > 32))) return KHB_EINVAL;
   if (c->in_flight) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
   if (c->d_gate) { hipFree(c->d_gate); c->d_gate = nullptr; }
-  c->gate_shift = 0;
+  c->gate_mask = 0;
   if (!gate) return KHB_OK;
   const size_t bytes = (size_t)1 << (log2_bits - 3);
   KHB_TRY(c, hipMalloc(&c->d_gate, bytes));
   KHB_TRY(c, hipMemcpy(c->d_gate, gate, bytes, hipMemcpyHostToDevice));
-  c->gate_shift = 64 - log2_bits;
+  c->gate_mask = (uint32_t)((1ull << log2_bits) - 1);
   return KHB_OK;
 }
 
@@ -1094,7 +1112,7 @@ int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t
   int rc = check_scan_args(c, centres, n_jobs, 0, groups_per_job, false);
   if (rc) return rc;
   if (!bytes_per_sub || !bits_per_sub || !hashes) return KHB_EINVAL;
-  if (gate && (gate_log2 < 13 || gate_log2 > 40)) return KHB_EINVAL;
+  if (gate && (gate_log2 < 13 || gate_log2 > 32)) return KHB_EINVAL;
   uint8_t* outs[3] = {l1, l2, l3};
   for (int l = 0; l < 3; ++l)
     if (outs[l] && (bits_per_sub[l] < 2 || (bits_per_sub[l] + 7) / 8 != bytes_per_sub[l] || hashes[l] == 0 ||
@@ -1119,7 +1137,7 @@ int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t
     if (e == hipSuccess) e = hipMemsetAsync(dgate, 0, gate_bytes, c->stream);
     A.gate_w = dgate;
     A.glimit = l1ext;
-    A.gate_shift = 64 - gate_log2;
+    A.gate_mask = (uint32_t)((1ull << gate_log2) - 1);
   }
   for (int l = 0; l < 3 && e == hipSuccess; ++l) {
     if (!outs[l]) continue;

@@ -172,7 +172,7 @@ def _l1_check(bf: bytes, nb: int, bits: int, hashes: int, xb: bytes, ora) -> boo
 
 def test_gate_candidates_exact(eng, bs32, ora):
     """Level-0 gate (khb_load_gate): the candidates are exactly the giant steps whose x passes the
-    level-1 bloom AND whose gate bit XXH64(x) >> (64 - log2) is set.  A dense synthetic L1 (each bit
+    level-1 bloom AND whose gate bit x mod 2^log2 is set.  A dense synthetic L1 (each bit
     set with p = 0.97, so ~54 % of all x pass) and a random half-full gate exercise both paths on
     every x of four chunks; without the gate the same scan returns the plain L1 candidates."""
     gpl = 4
@@ -193,7 +193,7 @@ def test_gate_candidates_exact(eng, bs32, ora):
             xb = xs[32 * a:32 * a + 32]
             if _l1_check(bf, nb, bits, hashes, xb, ora):
                 l1.append(a)
-                g = ora.xxh64(xb, 0x59F2815B16F81798) >> (64 - lg)
+                g = int.from_bytes(xb, "big") & ((1 << lg) - 1)
                 if (gate[g >> 3] >> (g & 7)) & 1:
                     gt.append(a)
         l1_ref.append(l1)
