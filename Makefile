@@ -75,3 +75,12 @@ $(LIBDIR)/variants/libkhbsgs_p%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) -DKHB_PROBE_MODE=$* -shared -o $@ $(CSRC)/khbsgs.hip
 .PHONY: variants
+$(LIBDIR)/variants/libkhbsgs_q%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_PIPE=$* -shared -o $@ $(CSRC)/khbsgs.hip
+$(LIBDIR)/variants/libkhbsgs_b%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_BATCH=$* -shared -o $@ $(CSRC)/khbsgs.hip
+$(LIBDIR)/variants/libkhbsgs_f%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_FUSE=$* -shared -o $@ $(CSRC)/khbsgs.hip

@@ -2,9 +2,10 @@
 """bench.py — BSGS giant-step throughput on puzzle #66 (BASELINE.json configs[1]: -b 66, k=1).
 
 One step = one GPU scan batch of the product search (libkhhost -> libkhbsgs): host centres for
-256 chunks, the HIP giant-step kernel over all 4096 groups of each chunk (256 x 4096 x 1024 =
-2^30 giant steps; at k=4, 1024 chunks x 1024 groups), and the CPU confirmation of every level-1
-candidate, pipelined exactly as the keyhunt_amd CLI runs it.  Tables are built and resident in HBM
+512 chunks, the HIP giant-step kernel over all 4096 groups of each chunk (512 x 4096 x 1024 =
+2^31 giant steps: one 8-group work item per lane of a full residency; at k=4, 2048 chunks x 1024
+groups), and the CPU confirmation of every level-1 candidate, pipelined exactly as the keyhunt_amd
+CLI runs it.  Tables are built and resident in HBM
 before the timed region.  Chunks are sequential 2N-key chunks of -b 66 starting right after the
 chunk holding puzzle #66's (public) key, so the search never stops early on the find and every
 rank times exactly K steps.  Multi-GPU: one process per GPU (torch.distributed.run), rank r owns
@@ -62,12 +63,12 @@ def cpu_baseline(seconds: float, threads: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # default: >= 30 s of steady state — 700 steps x 2^30 giant steps at ~44 ms
-    ap.add_argument("--steps", type=int, default=700)
+    # default: >= 30 s of steady state — 600 steps x 2^31 giant steps at ~54 ms
+    ap.add_argument("--steps", type=int, default=600)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--chunks", type=int, default=0,
-                    help="chunks (2N keys each) per step; default: 2^30 giant steps per step (256 at k=1, "
-                         "1024 at k=4), enough work items to fill every lane")
+                    help="chunks (2N keys each) per step; default: the fewest chunks that give every lane of "
+                         "the device one work item (512 at k=1, 2048 at k=4), at least 2^30 giant steps")
     ap.add_argument("--k", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -90,7 +91,10 @@ def main():
     tables = khhost.Tables(None, args.k, threads=host_threads, gpl=4)
     t_build = time.time() - t0
     if not args.chunks:
-        args.chunks = max(1, (1 << 30) // (tables.cycles * 1024))
+        # >= 2^30 giant steps per step, and enough work items to give every lane one
+        from keyhuntm1cpu_amd import khbsgs
+        fill = -(-khbsgs.default_lanes(local) * khbsgs.groups_per_item() // tables.cycles)
+        args.chunks = max(1, (1 << 30) // (tables.cycles * 1024), fill)
     target = puzzle66_target()
     two_n = 2 * (tables.n_low)                     # 2N keys per chunk
     key_chunk = (PUZZLE66_KEY - (1 << 65)) // two_n

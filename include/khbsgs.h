@@ -71,8 +71,14 @@ const char* khb_strerror(int code);
 int khb_last_hip_error(const khb_ctx* ctx);
 /* The hipStream_t the context launches on (for external HIP events / synchronisation). */
 void* khb_stream(khb_ctx* ctx);
-/* Persistent-grid size of the context in work lanes (one lane = groups_per_lane groups at a time). */
+/* Persistent-grid size of the context in work lanes (one lane = one work item at a time). */
 uint32_t khb_lanes(const khb_ctx* ctx);
+/* The auto lane count khb_open(device, 0, ...) would choose (0 if the device is unusable). */
+uint32_t khb_default_lanes(int device);
+/* Groups per work item of the -m bsgs scan (khb_submit / khb_dump_x): a lane walks this many
+ * consecutive groups of one job with two field inversions in total, so a launch fills the device
+ * when n_jobs * ceil(group_count / khb_groups_per_item()) >= khb_lanes(ctx). */
+uint32_t khb_groups_per_item(void);
 
 /* ---- tables (bsgs setup, keyhunt.cpp:1185-1364) ---- */
 /* Level-1 bloom: 256 sub-blooms of identical geometry concatenated in sub-bloom order

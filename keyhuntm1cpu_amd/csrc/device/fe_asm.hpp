@@ -394,6 +394,10 @@ FM_DEV void fm_sqr512x(uint32_t t[16], const uint32_t* a) {
   for (int i = 0; i < 16; ++i) t[i] = u[i];
 }
 
+// Second stage of the reduction: T = L + (H << 32) (+ addend) as 10 words with T9:T8 <= 2^32 + 1,
+// H = the high half of the product; returns a value < 2^256 congruent to T + 977*H.
+FM_DEV void fm_reduce_T(Fe& r, const uint32_t T[10], const uint32_t* H);
+
 // Reduce t (512 bits) mod p to a value < 2^256 (lazy).  2^256 = 2^32 + 977 (mod p).
 FM_DEV void fm_reduce(Fe& r, const uint32_t t[16]) {
   const uint32_t* L = t;
@@ -423,6 +427,67 @@ FM_DEV void fm_reduce(Fe& r, const uint32_t t[16]) {
       : "v"(L[0]), "v"(L[1]), "v"(L[2]), "v"(L[3]), "v"(L[4]), "v"(L[5]), "v"(L[6]), "v"(L[7]),
         "v"(H[0]), "v"(H[1]), "v"(H[2]), "v"(H[3]), "v"(H[4]), "v"(H[5]), "v"(H[6]), "v"(H[7]), "v"(0u)
       : "vcc");
+  fm_reduce_T(r, T, H);
+}
+
+// (t + w) mod p, lazy (< 2^256), for t a 512-bit product and any w < 2^256: the addend rides in
+// the reduction's first carry chain, so a following modular add/sub (x = s^2 - u) costs 9
+// instructions instead of 19.  T = (L + w) + (H << 32) < 2^288 + 2^257: T9:T8 <= 2^32 + 1, the
+// same bound fm_reduce_T relies on.
+FM_DEV void fm_reduce_add(Fe& r, const uint32_t t[16], const Fe& w) {
+  const uint32_t* L = t;
+  const uint32_t* H = t + 8;
+  uint32_t U[9], T[10];
+  asm("v_add_co_u32_e32 %0, vcc, %9, %17\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %10, %18, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %11, %19, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %12, %20, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %13, %21, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %14, %22, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %15, %23, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %16, %24, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %8, vcc, 0, %25, vcc"
+      : "=&v"(U[0]), "=&v"(U[1]), "=&v"(U[2]), "=&v"(U[3]), "=&v"(U[4]), "=&v"(U[5]), "=&v"(U[6]), "=&v"(U[7]),
+        "=&v"(U[8])
+      : "v"(L[0]), "v"(L[1]), "v"(L[2]), "v"(L[3]), "v"(L[4]), "v"(L[5]), "v"(L[6]), "v"(L[7]),
+        "v"(w.v[0]), "v"(w.v[1]), "v"(w.v[2]), "v"(w.v[3]), "v"(w.v[4]), "v"(w.v[5]), "v"(w.v[6]), "v"(w.v[7]),
+        "v"(0u)
+      : "vcc");
+  T[0] = U[0];
+  asm("v_add_co_u32_e32 %0, vcc, %9, %17\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %10, %18, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %11, %19, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %12, %20, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %13, %21, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %14, %22, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %15, %23, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %16, %24, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %8, vcc, 0, %25, vcc"
+      : "=&v"(T[1]), "=&v"(T[2]), "=&v"(T[3]), "=&v"(T[4]), "=&v"(T[5]), "=&v"(T[6]), "=&v"(T[7]), "=&v"(T[8]),
+        "=&v"(T[9])
+      : "v"(U[1]), "v"(U[2]), "v"(U[3]), "v"(U[4]), "v"(U[5]), "v"(U[6]), "v"(U[7]), "v"(U[8]),
+        "v"(H[0]), "v"(H[1]), "v"(H[2]), "v"(H[3]), "v"(H[4]), "v"(H[5]), "v"(H[6]), "v"(H[7]), "v"(0u)
+      : "vcc");
+  fm_reduce_T(r, T, H);
+}
+
+FM_DEV void fm_reduce_T(Fe& r, const uint32_t T[10], const uint32_t* H) {
   // P_i = 977*H_i + T_i  (< 2^42), independent
   uint64_t P[8];
 #pragma unroll
@@ -533,6 +598,19 @@ FM_DEV void fm_sqr(Fe& r, const Fe& a) {
   fm_reduce(r, t);
 }
 
+// r = a^2 + w (mod p), lazy; w < 2^256 (fm_reduce_add).
+FM_DEV void fm_sqr_add(Fe& r, const Fe& a, const Fe& w) {
+  uint32_t t[16];
+#if KHB_SQR_IMPL == 0
+  fm_mul512(t, a.v, a.v);
+#elif KHB_SQR_IMPL == 1
+  fm_sqr512x(t, a.v);
+#else
+  fm_sqr512p(t, a.v);
+#endif
+  fm_reduce_add(r, t, w);
+}
+
 // Previous schedule (column shuffle, squaring as a general product), kept as the
 // microbenchmark / exactness baseline (tools/microbench/fmbench.hip).
 FM_DEV void fm_mul_shuffle(Fe& r, const Fe& a, const Fe& b) {
@@ -629,6 +707,53 @@ FM_DEV void fm_canon(Fe& r, const Fe& a) {
   const bool sel = c != 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) r.v[i] = sel ? t[i] : a.v[i];
+}
+
+// a + b mod p, lazy: for a < p and b < 2^256 (so a + b < 2^257 - 0x1000003D1) the sum folds its
+// carry back as 2^256 = 0x1000003D1 (mod p) and stays < 2^256.  Feeds a product only.
+FM_DEV void fm_add_lazy(Fe& r, const Fe& a, const Fe& b) {
+  uint32_t s[8], c, k0;
+  asm("v_add_co_u32_e32 %0, vcc, %10, %18\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %11, %19, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %12, %20, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %13, %21, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %14, %22, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %15, %23, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %16, %24, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %17, %25, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %8, vcc, 0, %26, vcc\n\t"     // c = carry (0/1)
+      "v_mul_u32_u24_e32 %9, 0x3d1, %8\n\t"            // c * 977
+      "v_add_co_u32_e32 %0, vcc, %0, %9\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %1, %8, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %4, vcc, 0, %4, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %5, vcc, 0, %5, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %7, vcc, 0, %7, vcc"
+      : "=&v"(s[0]), "=&v"(s[1]), "=&v"(s[2]), "=&v"(s[3]), "=&v"(s[4]), "=&v"(s[5]), "=&v"(s[6]), "=&v"(s[7]),
+        "=&v"(c), "=&v"(k0)
+      : "v"(a.v[0]), "v"(a.v[1]), "v"(a.v[2]), "v"(a.v[3]), "v"(a.v[4]), "v"(a.v[5]), "v"(a.v[6]), "v"(a.v[7]),
+        "v"(b.v[0]), "v"(b.v[1]), "v"(b.v[2]), "v"(b.v[3]), "v"(b.v[4]), "v"(b.v[5]), "v"(b.v[6]), "v"(b.v[7]),
+        "v"(0u)
+      : "vcc");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = s[i];
 }
 
 // a + b mod p, a, b < p, canonical result

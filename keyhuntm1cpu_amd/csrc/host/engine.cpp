@@ -144,8 +144,9 @@ void confirm(Shared& S, const Batch& b, std::vector<khb_cand>& cands, int thread
 
 uint32_t batch_chunks(const Tables& T, const SearchConfig& cfg, size_t ntargets, uint32_t ctx_lanes) {
   if (cfg.chunks_per_batch) return cfg.chunks_per_batch;
-  const uint64_t lanes_per_job = (T.geo.cycles + T.gpl - 1) / T.gpl;
-  const uint64_t lanes = ctx_lanes ? ctx_lanes : 256u * 8u * 64u;
+  const uint64_t per_item = khb_groups_per_item();
+  const uint64_t lanes_per_job = (T.geo.cycles + per_item - 1) / per_item;
+  const uint64_t lanes = ctx_lanes ? ctx_lanes : 256u * 16u * 64u;
   const uint64_t jobs = (2ull * lanes + lanes_per_job - 1) / lanes_per_job;    // ~2 work items per lane
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(jobs / std::max<size_t>(1, ntargets), 65536));
 }

@@ -40,10 +40,20 @@ struct AffPt {
 #ifndef KHB_GSN_SCALAR
 #define KHB_GSN_SCALAR 1          // GSn table through scalar loads
 #endif
+#ifndef KHB_PIPE
+#define KHB_PIPE 1                // walk_group software pipelining (bit 0 prefix prefetch, bit 1 paired gate loads)
+#endif
+#ifndef KHB_FUSE
+#define KHB_FUSE 1                // -m bsgs walk: x = s^2 + nu fused into the squaring's reduction
+#endif
 #ifndef KHB_WAVES_PER_SIMD
 #define KHB_WAVES_PER_SIMD 4      // occupancy target of k_giant_scan (launch bounds); w4 measured best
 #endif
 constexpr uint32_t kBlock = 256;
+#ifndef KHB_BATCH
+#define KHB_BATCH 8               // -m bsgs groups per work item (scan_batch): two inversions per item
+#endif
+constexpr uint32_t kBatch = KHB_BATCH;
 
 // Kernel modes (template argument of scan_group / k_giant_scan).
 enum : int {
@@ -68,6 +78,7 @@ struct ScanArgs {
   BloomGeom geom;
   const AffPt* __restrict__ gsn;       // [0..511] GSn, [512] _2GSn
   const AffPt* __restrict__ offs;      // lane start offsets
+  const AffPt* __restrict__ gofs;      // per-group centre offsets j*_2GSn (scan_batch)
   const AffPt* __restrict__ centres;   // per-job group-0 centre
   Fe* __restrict__ scratch;            // prefix products [512][lanes]
   khb_cand* __restrict__ cand;
@@ -371,67 +382,73 @@ __device__ __forceinline__ void x_out(const ScanArgs& A, Fe& x) {
   }
 }
 
-// One reference group centred on C; advances C to the next centre.  For -m bsgs this is
-// keyhunt.cpp:3873-3999 (table GSn, x only); for -m address it is keyhunt.cpp:2586-2711 with the
-// table Gn (same point order t = 0..1023, pts[t] = key + t), plus y where the search needs it.
-// C is canonical on entry and exit; products are lazy (< 2^256) and every x (and y) is
-// canonicalised before it is hashed or dumped (fe_asm.hpp value contract).
+// The 1023 x-only additions C -/+ GSn[i] and the centre of one reference group, in the
+// reference's backward order (keyhunt.cpp:3873-3943 / 2586-2711), given inv = the inverse of
+// prod_{i<512} (GSn[i].x - C.x) and the forward prefix products in scr[0..510] (stride lanes).
+// C is canonical; products are lazy (< 2^256) and every x (and y) is canonicalised before it is
+// hashed or dumped (fe_asm.hpp value contract).
 template <int MODE>
-__device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, AffPt& C, uint32_t job, uint32_t j,
-                                           Fe* scr) {
+__device__ __forceinline__ void walk_group(const ScanArgs& A, ProbeQueue& Q, const AffPt& C, Fe inv, uint32_t job,
+                                           uint32_t j, const Fe* scr) {
   constexpr bool DUMP = MODE == kDump;
   const uint32_t S = A.stride;
-  // GSn rows are wave-uniform: read them through the constant address space so they arrive by
-  // scalar loads (SGPRs, lgkmcnt) instead of occupying 16 VGPRs and the vector-memory queue.
   const GsnTable gsn{A.gsn};
-  Fe acc, dx;
-  // forward pass: prefix products of dx[i] = GSn[i].x - C.x (i < 512) and _2GSn.x - C.x
-  {
-    const Fe gx = gsn.x(0);
-    fm_sub(acc, gx, C.x);
+  Fe pre, dx;
+  // KHB_PIPE bit 0: the prefix for step i-1 is loaded during step i, so its HBM latency hides
+  // behind a whole step's arithmetic instead of being waited for right after the load.
+  constexpr bool PREFETCH = (KHB_PIPE & 1) && MODE == kScan;
+  Fe pre_next;
+  if (PREFETCH) pre_next = scr[(size_t)(kHalf - 2) * S];
+  // KHB_FUSE (-m bsgs x-only walks): C.x is carried as negCx = p - C.x, so dx = GSn.x + negCx and
+  // x = s^2 + (negCx - GSn.x) need no separate modular subtraction of the centre.
+  constexpr bool FUSED = KHB_FUSE && (MODE == kScan || MODE == kDump);
+  Fe negCx;
+  if constexpr (FUSED) {
+    Fe p;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p.v[k] = k == 0 ? KHB_P0 : (k == 1 ? KHB_P1 : 0xFFFFFFFFu);
+    fm_sub(negCx, p, C.x);
   }
-  scr[0] = acc;
-  for (uint32_t i = 1; i < kHalf; ++i) {
-    const Fe gx = gsn.x(i);
-    fm_sub(dx, gx, C.x);
-    fm_mul(acc, acc, dx);
-    scr[(size_t)i * S] = acc;
-  }
-  {
-    const Fe gx = gsn.x(kHalf);
-    fm_sub(dx, gx, C.x);
-  }
-  fm_mul(acc, acc, dx);
-  Fe accc;
-  fm_canon(accc, acc);
-  const bool degenerate = fe_is_zero(accc);
-  Fe inv;
-  fm_inv(inv, acc);                       // == 0 (mod p) when degenerate -> every inverse 0, as the reference
-  // i = 512: inverse of _2GSn.x - C.x, kept for the next centre
-  Fe pre;
-  {
-    // i = 512's inverse is only needed for the next centre: park it in prefix slot 511, which
-    // is read exactly once (here), instead of holding 8 VGPRs through the backward loop.
-    Fe inv2;
-    pre = scr[(size_t)(kHalf - 1) * S];
-    fm_mul(inv2, inv, pre);
-    scr[(size_t)(kHalf - 1) * S] = inv2;
-    asm volatile("" ::: "memory");
-  }
-  fm_mul(inv, inv, dx);
   for (int i = (int)kHalf - 1; i >= 0; --i) {
     Fe idx;
     if (i > 0) {
-      pre = scr[(size_t)(i - 1) * S];
+      if (PREFETCH) {
+        pre = pre_next;
+        if (i > 1) pre_next = scr[(size_t)(i - 2) * S];
+      } else {
+        pre = scr[(size_t)(i - 1) * S];
+      }
       fm_mul(idx, inv, pre);
       const Fe gx = gsn.x(i);
-      fm_sub(dx, gx, C.x);
+      if constexpr (FUSED) fm_add_lazy(dx, gx, negCx); else fm_sub(dx, gx, C.x);
       fm_mul(inv, inv, dx);
     } else {
       idx = inv;
     }
     Fe u, s, x1, y1;
     const AffPt g = gsn.pt(i);
+    if constexpr (FUSED) {
+      // x = s^2 + nu, nu = -(C.x + GSn.x): the addend rides in the squaring's reduction
+      // (fm_sqr_add), and s = (GSn.y + C.y)*dx^-1 takes a lazy sum (it only feeds a product).
+      fm_sub(u, negCx, g.x);
+      fm_add_lazy(s, g.y, C.y);
+      fm_mul(s, s, idx);
+      fm_sqr_add(x1, s, u);
+      x_out<MODE>(A, x1);
+      if (i < (int)kHalf - 1) {
+        Fe x2;
+        fm_sub(s, g.y, C.y);
+        fm_mul(s, s, idx);
+        fm_sqr_add(x2, s, u);
+        x_out<MODE>(A, x2);
+        if constexpr ((KHB_PIPE & 2) && MODE == kScan)
+          asm volatile("" ::"v"(x1.v[0]), "v"(x2.v[0]), "v"(x1.v[7]), "v"(x2.v[7]) : "memory");
+        probe_pair<DUMP>(A, Q, x1, x2, job, j, kHalf - 1 - (uint32_t)i, kHalf + 1 + (uint32_t)i);
+      } else {
+        probe<DUMP>(A, Q, x1, job, j, kHalf - 1 - (uint32_t)i);
+      }
+      continue;
+    }
     fm_add(u, C.x, g.x);                  // x = s^2 - (C.x + GSn.x)
     // C - GSn[i]: s = (-GSn.y - C.y)/dx; x needs only s^2, and with s' = -s = (GSn.y + C.y)/dx
     // y = (GSn.x - x)*s + GSn.y = (x - GSn.x)*s' + GSn.y   (keyhunt.cpp:2628-2641)
@@ -468,6 +485,8 @@ __device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, Aff
         addr_point<MODE>(A, x1, y1, job, j, kHalf - 1 - (uint32_t)i);
         addr_point<MODE>(A, x2, y2, job, j, kHalf + 1 + (uint32_t)i);
       } else {
+        if constexpr ((KHB_PIPE & 2) && MODE == kScan)   // both x before either gate load is issued
+          asm volatile("" ::"v"(x1.v[0]), "v"(x2.v[0]), "v"(x1.v[7]), "v"(x2.v[7]) : "memory");
         probe_pair<DUMP>(A, Q, x1, x2, job, j, kHalf - 1 - (uint32_t)i, kHalf + 1 + (uint32_t)i);
       }
     } else {
@@ -485,6 +504,53 @@ __device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, Aff
     addr_point<MODE>(A, C.x, C.y, job, j, kHalf);
   else
     probe<DUMP>(A, Q, C.x, job, j, kHalf);
+}
+
+// One reference group centred on C, walked on its own (-m address, baby steps): the 513-element
+// batch of IntGroup.cpp:36-58 including dx[512] = _2GSn.x - C.x, whose inverse advances C to the
+// next centre (keyhunt.cpp:3986-3999).  For -m address this is keyhunt.cpp:2586-2711 with the
+// table Gn (same point order t = 0..1023, pts[t] = key + t), plus y where the search needs it.
+template <int MODE>
+__device__ __forceinline__ void scan_group(const ScanArgs& A, ProbeQueue& Q, AffPt& C, uint32_t job, uint32_t j,
+                                           Fe* scr) {
+  const uint32_t S = A.stride;
+  // GSn rows are wave-uniform: read them through the constant address space so they arrive by
+  // scalar loads (SGPRs, lgkmcnt) instead of occupying 16 VGPRs and the vector-memory queue.
+  const GsnTable gsn{A.gsn};
+  Fe acc, dx;
+  // forward pass: prefix products of dx[i] = GSn[i].x - C.x (i < 512) and _2GSn.x - C.x
+  {
+    const Fe gx = gsn.x(0);
+    fm_sub(acc, gx, C.x);
+  }
+  scr[0] = acc;
+  for (uint32_t i = 1; i < kHalf; ++i) {
+    const Fe gx = gsn.x(i);
+    fm_sub(dx, gx, C.x);
+    fm_mul(acc, acc, dx);
+    scr[(size_t)i * S] = acc;
+  }
+  {
+    const Fe gx = gsn.x(kHalf);
+    fm_sub(dx, gx, C.x);
+  }
+  fm_mul(acc, acc, dx);
+  Fe accc;
+  fm_canon(accc, acc);
+  const bool degenerate = fe_is_zero(accc);
+  Fe inv;
+  fm_inv(inv, acc);                       // == 0 (mod p) when degenerate -> every inverse 0, as the reference
+  {
+    // i = 512's inverse is only needed for the next centre: park it in prefix slot 511, which
+    // is read exactly once (here), instead of holding 8 VGPRs through the backward loop.
+    Fe inv2;
+    const Fe pre = scr[(size_t)(kHalf - 1) * S];
+    fm_mul(inv2, inv, pre);
+    scr[(size_t)(kHalf - 1) * S] = inv2;
+    asm volatile("" ::: "memory");
+  }
+  fm_mul(inv, inv, dx);
+  walk_group<MODE>(A, Q, C, inv, job, j, scr);
   // next centre: C + _2GSn with y (keyhunt.cpp:3986-3999)
   {
     asm volatile("" ::: "memory");
@@ -531,9 +597,194 @@ __device__ __forceinline__ bool add_direct(AffPt& r, const AffPt& p1, const AffP
   return degenerate;
 }
 
+__device__ __forceinline__ Fe fe_small(uint32_t v) {
+  Fe r;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r.v[k] = k ? 0u : v;
+  return r;
+}
+
+// -m bsgs work item: groups [g0, g1) (at most kBatch) of one job with TWO field inversions in
+// total instead of one per group plus one per lane start:
+//  0. centres C_g = startP + gofs[g0+g] (gofs[j] = j*_2GSn), all from startP, batch-inverted
+//     together (Montgomery over the <= kBatch x-differences; AddDirect, SECP256K1.cpp:242-265);
+//  1. per group the forward prefix products of dx_i = GSn[i].x - C.x, i < 512, into scratch;
+//     the group totals T_g are chained into one product;
+//  2. one inversion of that product, split back into inv(T_g) (Montgomery again);
+//  3. per group the reference's backward walk (walk_group).
+// The reference's batch per group also holds dx[512] = _2GSn.x - C.x (the next-centre add); its
+// inverse is not needed here (centres come from step 0), but a group whose 513-element product is
+// zero gets all-zero inverses in the reference (IntGroup.cpp:36-58 + IntMod.cpp:497-500): such a
+// group is kept out of the chained product and walked with inv = 0, which reproduces its x values
+// bit for bit (and is reported, as scan_group does).
+// Scratch (lane-private, stride = lanes, 32 B entries): g*512 + i (i < 511) prefixes of group g,
+// g*512 + 511 = T_g then inv(T_g); kBatch*512 + 2g (+1) = C_g.x (.y); kBatch*514 + g = chained
+// products.
+template <int MODE>
+__device__ __forceinline__ void scan_batch(const ScanArgs& A, ProbeQueue& Q, uint32_t job, uint32_t g0, uint32_t g1,
+                                           Fe* scr) {
+  const size_t S = A.stride;
+  const GsnTable gsn{A.gsn};
+  const uint32_t nb = g1 - g0;
+  Fe* const sc = scr + (size_t)kBatch * kHalf * S;          // centres
+  Fe* const sq = scr + (size_t)kBatch * (kHalf + 2) * S;    // chained products
+  const AffPt P = A.centres[job];
+  // 0. centres
+  uint32_t skip = 0;      // bit g: no add (group 0 is startP) or a degenerate add (gofs.x == P.x)
+  Fe acc;
+  for (uint32_t g = 0; g < nb; ++g) {
+    const uint32_t jg = g0 + g;
+    Fe d = fe_small(1);
+    if (jg != 0) {
+      fm_sub(d, A.gofs[jg].x, P.x);
+      Fe dc;
+      fm_canon(dc, d);
+      if (fe_is_zero(dc)) {
+        d = fe_small(1);
+        skip |= 1u << g;
+        if (MODE != kDump) {
+          const uint32_t k = atomicAdd(&A.counters[1], 1u);
+          if (k < A.degen_cap) A.degen[k] = khb_degenerate{job, jg | 0x80000000u};
+        }
+      }
+    } else {
+      skip |= 1u << g;
+    }
+    if (g == 0) acc = d; else fm_mul(acc, acc, d);
+    sq[g * S] = acc;
+  }
+  Fe inv;
+  fm_inv(inv, acc);
+  for (int g = (int)nb - 1; g >= 0; --g) {
+    const uint32_t jg = g0 + (uint32_t)g;
+    const AffPt O = A.gofs[jg];
+    Fe ig;
+    if (g > 0) {
+      fm_mul(ig, inv, sq[(g - 1) * S]);
+      Fe d = fe_small(1);
+      if (!((skip >> g) & 1u)) fm_sub(d, O.x, P.x);
+      fm_mul(inv, inv, d);
+    } else {
+      ig = inv;
+    }
+    AffPt C = P;
+    if (jg != 0) {
+      if ((skip >> g) & 1u) ig = fe_small(0);      // as add_direct: inverse of 0 is 0
+      Fe s, x, y;
+      fm_sub(s, O.y, P.y);
+      fm_mul(s, s, ig);
+      fm_sqr(x, s);
+      fm_sub(x, x, P.x);
+      fm_sub(x, x, O.x);
+      fm_canon(x, x);
+      fm_sub(y, O.x, x);
+      fm_mul(y, y, s);
+      fm_sub(y, y, O.y);
+      fm_canon(y, y);
+      C.x = x;
+      C.y = y;
+    }
+    sc[2 * g * S] = C.x;
+    sc[(2 * g + 1) * S] = C.y;
+  }
+  // 1. forward passes
+  const Fe g2x = gsn.x(kHalf);
+  uint32_t degen = 0;
+  for (uint32_t g = 0; g < nb; ++g) {
+    Fe* const sg = scr + (size_t)g * kHalf * S;
+    const Fe cx = sc[2 * g * S];
+    Fe a, dx;
+    fm_sub(a, gsn.x(0), cx);
+    sg[0] = a;
+    for (uint32_t i = 1; i < kHalf - 1; ++i) {
+      fm_sub(dx, gsn.x(i), cx);
+      fm_mul(a, a, dx);
+      sg[i * S] = a;
+    }
+    fm_sub(dx, gsn.x(kHalf - 1), cx);
+    fm_mul(a, a, dx);
+    Fe ac;
+    fm_canon(ac, a);
+    if (fe_is_zero(ac) || fe_eq(g2x, cx)) {
+      degen |= 1u << g;
+      a = fe_small(1);
+    }
+    sg[(kHalf - 1) * S] = a;
+    if (g == 0) acc = a; else fm_mul(acc, acc, a);
+    sq[g * S] = acc;
+  }
+  // 2. one inversion for the batch
+  fm_inv(inv, acc);
+  for (int g = (int)nb - 1; g >= 0; --g) {
+    Fe* const sg = scr + (size_t)g * kHalf * S;
+    Fe ig;
+    if (g > 0) {
+      fm_mul(ig, inv, sq[(g - 1) * S]);
+      fm_mul(inv, inv, sg[(kHalf - 1) * S]);
+    } else {
+      ig = inv;
+    }
+    if ((degen >> g) & 1u) ig = fe_small(0);
+    sg[(kHalf - 1) * S] = ig;
+  }
+  // 3. backward walks
+  for (uint32_t g = 0; g < nb; ++g) {
+    Fe* const sg = scr + (size_t)g * kHalf * S;
+    asm volatile("" ::: "memory");
+    const AffPt C{sc[2 * g * S], sc[(2 * g + 1) * S]};
+    walk_group<MODE>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
+    if (MODE != kDump && ((degen >> g) & 1u)) {
+      const uint32_t k = atomicAdd(&A.counters[1], 1u);
+      if (k < A.degen_cap) A.degen[k] = khb_degenerate{job, g0 + g};
+    }
+  }
+}
+
+// Per-group centre offsets gofs[j] = j*_2GSn from lane offsets offs[m] = (m*gpl)*_2GSn:
+// gofs[m*gpl + k] = offs[m] + k*_2GSn (gofs[0] is unused: group 0's centre is startP).
+__global__ void k_expand_offsets(const AffPt* __restrict__ offs, uint32_t gpl, const AffPt* __restrict__ gsn,
+                                 AffPt* __restrict__ out, uint32_t n) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t m = j / gpl, k = j % gpl;
+  const AffPt D = gsn[kHalf];
+  AffPt p = offs[m];
+  uint32_t todo = k;
+  if (m == 0 && k) {
+    p = D;
+    todo = k - 1;
+  }
+  for (uint32_t t = 0; t < todo; ++t) {
+    if (fe_eq(p.x, D.x)) {      // p == D (small multiples never meet -D): DoubleDirect, SECP256K1.cpp:376-401
+      Fe x2, num, den, s, x, y;
+      fm_sqr(x2, p.x);
+      fm_canon(x2, x2);
+      fm_add(num, x2, x2);
+      fm_add(num, num, x2);
+      fm_add(den, p.y, p.y);
+      fm_inv(den, den);
+      fm_mul(s, num, den);
+      fm_canon(s, s);
+      fm_sqr(x, s);
+      fm_sub(x, x, p.x);
+      fm_sub(x, x, p.x);
+      fm_canon(x, x);
+      fm_sub(y, p.x, x);
+      fm_mul(y, y, s);
+      fm_sub(y, y, p.y);
+      fm_canon(y, y);
+      p = AffPt{x, y};
+    } else {
+      add_direct(p, p, D);
+    }
+  }
+  out[j] = p;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanArgs A) {
   constexpr bool QUEUE = MODE == kScan;
+  constexpr bool BATCH = MODE == kScan || MODE == kDump;
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   Fe* scr = A.scratch + lane;
   __shared__ uint32_t s_queue[QUEUE ? kWavesPerBlock : 1][QUEUE ? kQWords * kQCap : 1];
@@ -541,20 +792,30 @@ __global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanA
   const uint32_t wave = QUEUE ? threadIdx.x >> 6 : 0;
   ProbeQueue Q{s_queue[wave], &s_count[wave]};
   if (QUEUE) *Q.n = 0;
-  for (uint64_t item = lane; item < A.n_items; item += A.stride) {
-    const uint32_t job = (uint32_t)(item / A.lanes_per_job);
-    const uint32_t m = (uint32_t)(item % A.lanes_per_job);
-    const uint32_t g0 = A.group_begin + m * A.gpl;
-    const uint32_t g1 = min(g0 + A.gpl, A.group_end);
-    AffPt C = A.centres[job];
-    const uint32_t mo = g0 / A.gpl;
-    if (mo != 0) {
-      if (add_direct(C, C, A.offs[mo]) && !is_dump(MODE)) {
-        uint32_t k = atomicAdd(&A.counters[1], 1u);
-        if (k < A.degen_cap) A.degen[k] = khb_degenerate{job, g0 | 0x80000000u};
-      }
+  if constexpr (BATCH) {
+    for (uint64_t item = lane; item < A.n_items; item += A.stride) {
+      const uint32_t job = (uint32_t)(item / A.lanes_per_job);
+      const uint32_t m = (uint32_t)(item % A.lanes_per_job);
+      const uint32_t g0 = A.group_begin + m * kBatch;
+      const uint32_t g1 = min(g0 + kBatch, A.group_end);
+      scan_batch<MODE>(A, Q, job, g0, g1, scr);
     }
-    for (uint32_t j = g0; j < g1; ++j) scan_group<MODE>(A, Q, C, job, j, scr);
+  } else {
+    for (uint64_t item = lane; item < A.n_items; item += A.stride) {
+      const uint32_t job = (uint32_t)(item / A.lanes_per_job);
+      const uint32_t m = (uint32_t)(item % A.lanes_per_job);
+      const uint32_t g0 = A.group_begin + m * A.gpl;
+      const uint32_t g1 = min(g0 + A.gpl, A.group_end);
+      AffPt C = A.centres[job];
+      const uint32_t mo = g0 / A.gpl;
+      if (mo != 0) {
+        if (add_direct(C, C, A.offs[mo]) && !is_dump(MODE)) {
+          uint32_t k = atomicAdd(&A.counters[1], 1u);
+          if (k < A.degen_cap) A.degen[k] = khb_degenerate{job, g0 | 0x80000000u};
+        }
+      }
+      for (uint32_t j = g0; j < g1; ++j) scan_group<MODE>(A, Q, C, job, j, scr);
+    }
   }
   if (QUEUE) q_drain(A, Q, 1);   // the wave has reconverged: finish what is still queued
 }
@@ -613,6 +874,8 @@ struct khb_ctx {
   AffPt* d_gsn = nullptr;
   AffPt* d_offs = nullptr;
   uint32_t n_offs = 0, gpl = 0;
+  AffPt* d_gofs = nullptr;             // per-group offsets expanded from gpl > 1 lane offsets
+  bool gofs_stale = true;
   AffPt* d_centres = nullptr;
   uint32_t centres_cap = 0;
   Fe* d_scratch = nullptr;
@@ -660,14 +923,20 @@ int ensure_centres(khb_ctx* c, uint32_t n) {
   return KHB_OK;
 }
 
-ScanArgs make_args(khb_ctx* c, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count) {
+// Entries (32 B) of lane-private scratch: scan_group needs 512, scan_batch kBatch*514 + kBatch.
+constexpr size_t kScratchEntries = (size_t)kBatch * (kHalf + 3) > kHalf ? (size_t)kBatch * (kHalf + 3) : kHalf;
+
+// per_item: groups per work item (the lane-offset stride gpl, or kBatch for scan_batch modes)
+ScanArgs make_args(khb_ctx* c, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count, uint32_t per_item = 0) {
   ScanArgs A{};
+  if (per_item == 0) per_item = c->gpl;
   A.bloom = c->d_bloom;
   A.geom = c->geom;
   A.gate = c->d_gate;
   A.gate_mask = c->gate_mask;
   A.gsn = c->d_gsn;
   A.offs = c->d_offs;
+  A.gofs = c->gpl == 1 ? c->d_offs : c->d_gofs;
   A.centres = c->d_centres;
   A.scratch = c->d_scratch;
   A.cand = c->d_cand;
@@ -677,7 +946,7 @@ ScanArgs make_args(khb_ctx* c, uint32_t n_jobs, uint32_t group_begin, uint32_t g
   A.group_begin = group_begin;
   A.group_end = group_begin + group_count;
   A.gpl = c->gpl;
-  A.lanes_per_job = (group_count + c->gpl - 1) / c->gpl;
+  A.lanes_per_job = (group_count + per_item - 1) / per_item;
   A.n_items = (uint64_t)n_jobs * A.lanes_per_job;
   A.stride = c->lanes;
   A.cand_cap = kCandCap;
@@ -694,6 +963,21 @@ int check_scan_args(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_
   if (end > 0xFFFFFFFFull) return KHB_EINVAL;
   if (bsgs && end * KHB_GROUP > 0xFFFFFFFFull) return KHB_EINVAL;  // a = j*1024+t fits 32 bits (keyhunt.cpp:3948)
   if ((end + c->gpl - 1) / c->gpl > c->n_offs) return KHB_EINVAL;  // offsets table too short
+  return KHB_OK;
+}
+
+// Per-group centre offsets for scan_batch: the lane offsets themselves when gpl == 1, else
+// expanded once on the device (k_expand_offsets) after the giant table and offsets are loaded.
+int ensure_gofs(khb_ctx* c) {
+  if (c->gpl == 1 || !c->gofs_stale) return KHB_OK;
+  const uint32_t n = c->n_offs * c->gpl;
+  if (c->d_gofs) { hipFree(c->d_gofs); c->d_gofs = nullptr; }
+  KHB_TRY(c, hipMalloc(&c->d_gofs, sizeof(AffPt) * (size_t)n));
+  hipLaunchKernelGGL(k_expand_offsets, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->d_offs, c->gpl, c->d_gsn,
+                     c->d_gofs, n);
+  KHB_TRY(c, hipGetLastError());
+  KHB_TRY(c, hipStreamSynchronize(c->stream));
+  c->gofs_stale = false;
   return KHB_OK;
 }
 
@@ -717,6 +1001,16 @@ const char* khb_strerror(int code) {
 int khb_last_hip_error(const khb_ctx* c) { return c ? c->last_hip : 0; }
 void* khb_stream(khb_ctx* c) { return c ? (void*)c->stream : nullptr; }
 uint32_t khb_lanes(const khb_ctx* c) { return c ? c->lanes : 0; }
+uint32_t khb_groups_per_item(void) { return kBatch; }
+
+uint32_t khb_default_lanes(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return 0;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return 0;
+  return (uint32_t)prop.multiProcessorCount * 4u * KHB_WAVES_PER_SIMD * 64u;
+}
 
 int khb_device_count(int* n) {
   if (!n) return KHB_EINVAL;
@@ -745,7 +1039,7 @@ int khb_open(int device, uint32_t lanes, khb_ctx** out) {
   hipError_t e;
   if ((e = hipSetDevice(device)) != hipSuccess) return fail(e);
   if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e);
-  if ((e = hipMalloc(&c->d_scratch, sizeof(Fe) * (size_t)kHalf * lanes)) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&c->d_scratch, sizeof(Fe) * kScratchEntries * lanes)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&c->d_cand, sizeof(khb_cand) * kCandCap)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&c->d_degen, sizeof(khb_degenerate) * kDegenCap)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&c->d_counters, 16)) != hipSuccess) return fail(e);
@@ -764,6 +1058,7 @@ int khb_close(khb_ctx* c) {
   hipFree(c->d_gate);
   hipFree(c->d_gsn);
   hipFree(c->d_offs);
+  hipFree(c->d_gofs);
   hipFree(c->d_centres);
   hipFree(c->d_scratch);
   hipFree(c->d_cand);
@@ -819,6 +1114,7 @@ int khb_load_giant_table(khb_ctx* c, const uint8_t* gsn) {
   pts_from_be(h, gsn, KHB_GIANT_TABLE);
   if (!c->d_gsn) KHB_TRY(c, hipMalloc(&c->d_gsn, sizeof(h)));
   KHB_TRY(c, hipMemcpy(c->d_gsn, h, sizeof(h), hipMemcpyHostToDevice));
+  c->gofs_stale = true;
   return KHB_OK;
 }
 
@@ -836,6 +1132,7 @@ int khb_load_lane_offsets(khb_ctx* c, const uint8_t* offs, uint32_t n, uint32_t 
   if (e != hipSuccess) return hip_fail(c, e);
   c->n_offs = n;
   c->gpl = gpl;
+  c->gofs_stale = true;
   return KHB_OK;
 }
 
@@ -845,11 +1142,11 @@ int khb_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t gro
   if (!c->d_bloom) return KHB_ESTATE;
   if (c->in_flight || c->addr_in_flight) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
-  if ((rc = ensure_centres(c, n_jobs))) return rc;
+  if ((rc = ensure_centres(c, n_jobs)) || (rc = ensure_gofs(c))) return rc;
   pts_from_be(c->h_centres, centres, n_jobs);
   KHB_TRY(c, hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, c->stream));
   KHB_TRY(c, hipMemsetAsync(c->d_counters, 0, 16, c->stream));
-  ScanArgs A = make_args(c, n_jobs, group_begin, group_count);
+  ScanArgs A = make_args(c, n_jobs, group_begin, group_count, kBatch);
   const uint32_t blocks = c->lanes / kBlock;
   KHB_TRY(c, hipEventRecord(c->ev0, c->stream));
   hipLaunchKernelGGL(k_giant_scan<kScan>, dim3(blocks), dim3(kBlock), 0, c->stream, A);
@@ -898,7 +1195,7 @@ int khb_dump_x(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint32_t
   if (!xs) return KHB_EINVAL;
   if (c->in_flight) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
-  if ((rc = ensure_centres(c, 1))) return rc;
+  if ((rc = ensure_centres(c, 1)) || (rc = ensure_gofs(c))) return rc;
   pts_from_be(c->h_centres, centre, 1);
   const size_t bytes = (size_t)group_count * KHB_GROUP * 32;
   uint8_t* d_x = nullptr;
@@ -906,7 +1203,7 @@ int khb_dump_x(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint32_t
   hipError_t e = hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt), hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, 16, c->stream);
   if (e == hipSuccess) {
-    ScanArgs A = make_args(c, 1, group_begin, group_count);
+    ScanArgs A = make_args(c, 1, group_begin, group_count, kBatch);
     A.xdump = d_x;
     const uint32_t blocks = (uint32_t)((A.n_items + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_giant_scan<kDump>, dim3(blocks < c->lanes / kBlock ? blocks : c->lanes / kBlock),

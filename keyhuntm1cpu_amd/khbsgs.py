@@ -57,6 +57,10 @@ def lib(path: str | None = None) -> C.CDLL:
         L.khb_stream.argtypes = [C.c_void_p]
         L.khb_lanes.restype = C.c_uint32
         L.khb_lanes.argtypes = [C.c_void_p]
+        L.khb_default_lanes.restype = C.c_uint32
+        L.khb_default_lanes.argtypes = [C.c_int]
+        L.khb_groups_per_item.restype = C.c_uint32
+        L.khb_groups_per_item.argtypes = []
         L.khb_load_bloom.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, C.c_uint64, C.c_uint32]
         L.khb_load_giant_table.argtypes = [C.c_void_p, C.c_char_p]
         L.khb_load_gate.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32]
@@ -86,6 +90,16 @@ def _check(rc: int, ctx=None, L: C.CDLL | None = None) -> None:
         if ctx:
             msg += f" (hipError {L.khb_last_hip_error(ctx)})"
         raise KhbError(f"khbsgs: {msg} [{rc}]")
+
+
+def groups_per_item() -> int:
+    """Groups per work item of the -m bsgs scan kernel (khb_groups_per_item)."""
+    return int(lib().khb_groups_per_item())
+
+
+def default_lanes(device: int = 0) -> int:
+    """Work lanes of one full residency on `device` (khb_default_lanes; 0 = unusable)."""
+    return int(lib().khb_default_lanes(device))
 
 
 def device_count() -> int:
