@@ -118,8 +118,9 @@ int khb_scan(khb_ctx* ctx, const uint8_t* centres_xy_be, uint32_t n_jobs, uint32
  * group_begin+group_count) of ONE job; xs must hold group_count*1024*32 bytes. */
 int khb_dump_x(khb_ctx* ctx, const uint8_t* centre_xy_be, uint32_t group_begin, uint32_t group_count,
                uint8_t* xs);
-/* Field self-test kernel: r[i] = op(a[i], b[i]) for op 0=mul 1=sqr 2=add 3=sub 4=inv;
- * 32-byte BE values. */
+/* Field self-test kernel: r[i] = op(a[i], b[i]) mod p, canonical, for op 0=mul 1=sqr 2=add 3=sub
+ * 4=inv 5=lazy add (a < p, b < 2^256) 6=a^2 + b (the fused squaring, a, b < 2^256); 32-byte BE
+ * values. */
 int khb_field_op(khb_ctx* ctx, int op, const uint8_t* a, const uint8_t* b, uint8_t* r, uint32_t n);
 /* Bloom self-test kernel: hit[i] = bloom_check(level-1, x[i]) for 32-byte BE x values. */
 int khb_probe(khb_ctx* ctx, const uint8_t* xs, uint8_t* hit, uint32_t n);

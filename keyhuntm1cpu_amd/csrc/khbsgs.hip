@@ -43,6 +43,9 @@ struct AffPt {
 #ifndef KHB_PIPE
 #define KHB_PIPE 1                // walk_group software pipelining (bit 0 prefix prefetch, bit 1 paired gate loads)
 #endif
+#ifndef KHB_LDSCOUNT
+#define KHB_LDSCOUNT 1            // probe-queue count through an LDS-typed pointer (ds_* not flat_*)
+#endif
 #ifndef KHB_FUSE
 #define KHB_FUSE 1                // -m bsgs walk: x = s^2 + nu fused into the squaring's reduction
 #endif
@@ -131,7 +134,14 @@ constexpr uint32_t kWavesPerBlock = kBlock / 64;
 // a job, the tail of the item loop), and a register copy would go stale in the inactive lanes.
 struct ProbeQueue {
   uint32_t* q;            // this wave's LDS region: kQWords arrays of kQCap words
-  volatile uint32_t* n;   // this wave's queued-entry count (LDS)
+  // this wave's queued-entry count, typed as an LDS pointer: through a generic (flat) pointer
+  // every count access was a flat_load/flat_store, which counts against vmcnt AND lgkmcnt and
+  // made each one wait for all outstanding vector-memory operations (the prefetched prefix).
+#if KHB_LDSCOUNT
+  volatile __attribute__((address_space(3))) uint32_t* n;
+#else
+  volatile uint32_t* n;
+#endif
 };
 
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
@@ -790,7 +800,11 @@ __global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanA
   __shared__ uint32_t s_queue[QUEUE ? kWavesPerBlock : 1][QUEUE ? kQWords * kQCap : 1];
   __shared__ uint32_t s_count[kWavesPerBlock];
   const uint32_t wave = QUEUE ? threadIdx.x >> 6 : 0;
+#if KHB_LDSCOUNT
+  ProbeQueue Q{s_queue[wave], (volatile __attribute__((address_space(3))) uint32_t*)&s_count[wave]};
+#else
   ProbeQueue Q{s_queue[wave], &s_count[wave]};
+#endif
   if (QUEUE) *Q.n = 0;
   if constexpr (BATCH) {
     for (uint64_t item = lane; item < A.n_items; item += A.stride) {
@@ -848,6 +862,8 @@ __global__ void k_field_op(int op, const Fe* __restrict__ a, const Fe* __restric
     case 1: fm_sqr(z, x); break;
     case 2: fm_add(z, x, y); break;
     case 3: fm_sub(z, x, y); break;
+    case 5: fm_add_lazy(z, x, y); break;     // x < p, y < 2^256
+    case 6: fm_sqr_add(z, x, y); break;      // x, y < 2^256
     default: fm_inv(z, x); break;
   }
   fm_canon(z, z);
@@ -1218,7 +1234,7 @@ int khb_dump_x(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint32_t
 }
 
 int khb_field_op(khb_ctx* c, int op, const uint8_t* a, const uint8_t* b, uint8_t* r, uint32_t n) {
-  if (!c || !a || !r || n == 0 || op < 0 || op > 4 || (op != 1 && op != 4 && !b)) return KHB_EINVAL;
+  if (!c || !a || !r || n == 0 || op < 0 || op > 6 || (op != 1 && op != 4 && !b)) return KHB_EINVAL;
   KHB_TRY(c, hipSetDevice(c->device));
   Fe* h = (Fe*)malloc(sizeof(Fe) * n * 3);
   if (!h) return KHB_ENOMEM;

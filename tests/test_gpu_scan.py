@@ -58,6 +58,32 @@ def test_field_ops(eng):
         assert got == exp, f"field op {op}"
 
 
+def test_fused_field_ops(eng):
+    """The lazy add and the squaring with a fused addend (the x-only walk, KHB_FUSE) against Python
+    big integers, with operands up to 2^256 - 1 where the contract allows (fe_asm.hpp)."""
+    rng = random.Random(5)
+    n = 4096
+    lo = [0, 1, P - 1, P - 2, 2**255, 2**32 - 1]                    # < p
+    hi = lo + [P, P + 1, 2**256 - 1, 2**256 - 2, 2**256 - 2**32]     # < 2^256
+    a = [rand_fe(rng) for _ in range(n)]
+    b = [rng.randrange(2**256) for _ in range(n)]
+    k = 0
+    for x in hi:
+        for y in hi:
+            a[k], b[k] = x, y
+            k += 1
+    ab = b"".join(x.to_bytes(32, "big") for x in a)
+    bb = b"".join(x.to_bytes(32, "big") for x in b)
+    r = eng.field_op(6, ab, bb)
+    got = [int.from_bytes(r[32 * i:32 * i + 32], "big") for i in range(n)]
+    assert got == [(a[i] * a[i] + b[i]) % P for i in range(n)], "fm_sqr_add"
+    a2 = [x if x < P else x - P for x in a]                          # lazy add needs a < p
+    ab2 = b"".join(x.to_bytes(32, "big") for x in a2)
+    r = eng.field_op(5, ab2, bb)
+    got = [int.from_bytes(r[32 * i:32 * i + 32], "big") for i in range(n)]
+    assert got == [(a2[i] + b[i]) % P for i in range(n)], "fm_add_lazy"
+
+
 def test_probe_matches_oracle(eng, bs32, ora):
     load_tables(eng, bs32, 4)
     rng = random.Random(2)
