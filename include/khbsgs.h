@@ -85,13 +85,17 @@ uint32_t khb_groups_per_item(void);
  * (bloom_bP[0..255].bf, bloom.h:26-45).  bits/hashes as in struct bloom. */
 int khb_load_bloom(khb_ctx* ctx, const uint8_t* bf_concat, uint64_t bytes_per_sub, uint64_t bits_per_sub,
                    uint32_t hashes);
-/* Level-0 gate in front of the level-1 probe (no reference counterpart; a superset filter): a map of
- * 2^log2_bits bits, bit (x mod 2^log2_bits) set for every baby-step x of the level-1 set (x the
- * canonical x-coordinate as an integer; bit i of byte i/8, LSB first; khb_build_baby writes one).
- * With a gate, the giant-step probe reads the gate bit first and runs the level-1 check (both
- * XXH64, all bits) only when it is set: every level-1 candidate whose gate bit is set is still
- * reported, so no baby-step hit is lost.  gate NULL removes it; log2_bits in [13, 32]. */
-int khb_load_gate(khb_ctx* ctx, const uint8_t* gate, uint32_t log2_bits);
+/* Level-0 gate in front of the level-1 probe (no reference counterpart; a superset filter): a
+ * blocked bloom filter of 2^log2_bits bits in 64-bit blocks (block i = bytes 8i..8i+7, bit b of
+ * the block = bit b%8 of byte 8i + b/8).  With x the canonical x-coordinate as an integer,
+ * w0 = x mod 2^32 and w1 = (x >> 32) mod 2^32, x selects block w0 mod 2^(log2_bits-6) and within
+ * it bits (w1 >> 6p) mod 64, p < probes; every baby-step x of the level-1 set has its bits set
+ * (khb_build_baby writes one).  With a gate, the giant-step probe reads x's block (one 8-byte
+ * load) and runs the level-1 check (both XXH64, all bits) only when all its bits are set: every
+ * level-1 candidate that passes the gate is still reported, so no baby-step hit is lost.
+ * gate NULL removes it; log2_bits in [13, 32]; probes in [1, KHB_GATE_MAX_PROBES]. */
+#define KHB_GATE_MAX_PROBES 3
+int khb_load_gate(khb_ctx* ctx, const uint8_t* gate, uint32_t log2_bits, uint32_t probes);
 /* GSn[0..511] and _2GSn (keyhunt.cpp:1325-1338), 513 affine points x||y BE. */
 int khb_load_giant_table(khb_ctx* ctx, const uint8_t* gsn_xy_be);
 /* Lane start offsets: offs[m] = (m*groups_per_lane) * _2GSn, m in [0, n) (offs[0] unused: the
@@ -164,11 +168,11 @@ int khb_hash160(khb_ctx* ctx, int kind, const uint8_t* xy_be, uint8_t* out, uint
  * bsgs_xvalue {x bytes 16..21, 2 zero bytes, u64 ic} (unsorted).  l1/l2/l3 receive 256 concatenated
  * sub-blooms of bytes_per_sub[level] bytes (NULL skips a level, e.g. one read from -S files);
  * bp receives m3*16 bytes (NULL skips it).  gate (NULL skips it) receives the level-0 gate of
- * khb_load_gate for every ic < l1ext, 2^gate_log2 bits. */
+ * khb_load_gate for every ic < l1ext, 2^gate_log2 bits, gate_probes bits per x. */
 int khb_build_baby(khb_ctx* ctx, const uint8_t* centres_xy_be, uint32_t n_jobs, uint32_t groups_per_job,
                    uint64_t l1ext, uint64_t m2, uint64_t m3, const uint64_t bytes_per_sub[3],
                    const uint64_t bits_per_sub[3], const uint32_t hashes[3], uint8_t* l1, uint8_t* l2, uint8_t* l3,
-                   uint8_t* bp, uint8_t* gate, uint32_t gate_log2, float* kernel_ms);
+                   uint8_t* bp, uint8_t* gate, uint32_t gate_log2, uint32_t gate_probes, float* kernel_ms);
 
 #ifdef __cplusplus
 }

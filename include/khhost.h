@@ -44,6 +44,8 @@ void khh_amp_table(const khh_tables* t, int level, uint8_t out[32 * 64]);
 uint32_t khh_lane_offsets(const khh_tables* t, uint8_t* out /* n*64, may be NULL */, uint32_t* gpl);
 /* Level-0 gate (khb_load_gate): pointer to 2^log2 / 8 bytes, or NULL with *log2 = 0 when none */
 const uint8_t* khh_gate(const khh_tables* t, uint32_t* log2);
+/* Gate probes (bits per x, khb_load_gate's probes); 0 when the tables have no gate */
+uint32_t khh_gate_probes(const khh_tables* t);
 /* bPtable (sorted): m3 records of {6-byte value, 2 pad, u64 index} */
 const uint8_t* khh_bptable(const khh_tables* t, uint64_t* n);
 

@@ -163,7 +163,7 @@ static bool build_baby_gpu(Tables& T, const Geometry& g, const std::vector<Pt>& 
     rc = khb_build_baby(ctx, centres.data(), n_jobs, gpj, g.l1ext, g.m2, g.m3, bytes, bits, hashes,
                         need_l1 ? cat[0].data() : nullptr, need_l2 ? cat[1].data() : nullptr,
                         need_l3 ? cat[2].data() : nullptr, need_bp ? (uint8_t*)T.bp.data() : nullptr,
-                        gate_log2 ? T.gate.data() : nullptr, gate_log2, &ms);
+                        gate_log2 ? T.gate.data() : nullptr, gate_log2, T.gate_probes, &ms);
   khb_close(ctx);
   if (rc) {
     err = std::string("[E] GPU table build: ") + khb_strerror(rc);
@@ -175,6 +175,12 @@ static bool build_baby_gpu(Tables& T, const Geometry& g, const std::vector<Pt>& 
     if (!cat[l].empty())
       for (int i = 0; i < 256; ++i) memcpy((*lv[l])[i].bf.data(), cat[l].data() + i * bytes[l], bytes[l]);
   return true;
+}
+
+uint32_t Tables::gate_probes_for() {
+  uint32_t p = 3;
+  if (const char* e = getenv("KHB_GATE_PROBES")) p = (uint32_t)atoi(e);
+  return p < 1 ? 1 : (p > KHB_GATE_MAX_PROBES ? KHB_GATE_MAX_PROBES : p);
 }
 
 uint32_t Tables::gate_log2_for(const Geometry& g) {
@@ -214,6 +220,7 @@ bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, st
              need_bp = !(have & kFileBp);
   // level-0 gate: built wherever the whole L1 set is walked (the GPU walks it for the gate alone)
   gate_log2 = (need_l1 || gpu_device >= 0) ? gate_log2_for(g) : 0;
+  gate_probes = gate_log2 ? gate_probes_for() : 0;
   gate.assign(gate_log2 ? (size_t)1 << (gate_log2 - 3) : 0, 0);
   // baby steps to walk: all of the L1 extent, or only the first m2 when L1 came from a file
   const uint64_t extent = (need_l1 || (gate_log2 && gpu_device >= 0)) ? g.l1ext
@@ -299,10 +306,16 @@ bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, st
           if (need_l2 && ic < g.m2) l2[idx].add32_atomic(xb);
           if (need_l1 && ic < to) {
             l1[idx].add32_atomic(xb);
-            if (gate_log2) {   // bit x mod 2^gate_log2 (the low word of x: big-endian bytes 28..31)
-              const uint32_t lo = ((uint32_t)xb[28] << 24) | ((uint32_t)xb[29] << 16) | ((uint32_t)xb[30] << 8) | xb[31];
-              const uint32_t gb = lo & (uint32_t)((1ull << gate_log2) - 1);
-              __atomic_fetch_or(&gate[gb >> 3], (uint8_t)(1u << (gb & 7)), __ATOMIC_RELAXED);
+            // blocked gate (khb_load_gate): block w0 mod 2^(gate_log2-6), bits (w1 >> 6p) mod 64;
+            // w0 = x mod 2^32 is big-endian bytes 28..31, w1 = (x >> 32) mod 2^32 bytes 24..27
+            if (gate_probes) {
+              const uint32_t w0 = ((uint32_t)xb[28] << 24) | ((uint32_t)xb[29] << 16) | ((uint32_t)xb[30] << 8) | xb[31];
+              const uint32_t w1 = ((uint32_t)xb[24] << 24) | ((uint32_t)xb[25] << 16) | ((uint32_t)xb[26] << 8) | xb[27];
+              const uint64_t blk = w0 & (uint32_t)((1ull << (gate_log2 - 6)) - 1);
+              for (uint32_t p = 0; p < gate_probes; ++p) {
+                const uint32_t b = (w1 >> (6 * p)) & 63u;
+                __atomic_fetch_or(&gate[8 * blk + (b >> 3)], (uint8_t)(1u << (b & 7)), __ATOMIC_RELAXED);
+              }
             }
           }
         }

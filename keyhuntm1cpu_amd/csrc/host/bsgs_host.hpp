@@ -45,16 +45,18 @@ struct Tables {
   std::vector<XValue> bp;                // sorted by value (bsgs_sort)
   Pt gsn[512], g2sn, amp2[32], amp3[32];
   uint32_t gpl = 0;                      // GPU groups per lane
-  // Level-0 gate for the GPU probe (khb_load_gate): bit x mod 2^gate_log2 set for every
-  // x of the L1 set.  Built with the baby steps when the L1 set is walked (always on the GPU path;
-  // on the CPU path only when L1 is built, not read from a file); gate_log2 = 0: none.
+  // Level-0 gate for the GPU probe (khb_load_gate): a blocked bloom (64-bit blocks, gate_probes
+  // bits per x) holding every x of the L1 set.  Built with the baby steps when the L1 set is
+  // walked (always on the GPU path; on the CPU path only when L1 is built, not read from a file);
+  // gate_log2 = 0: none.
   std::vector<uint8_t> gate;
-  uint32_t gate_log2 = 0;
-  // Gate size for a geometry: 2^KHB_GATE_SPARSITY (default 64) bits per L1 x rounded up to a power
-  // of two, at most 2^30 bits (128 MiB) or 2^KHB_GATE_LOG2 from the environment (0 disables); 0
-  // when the map would be more than ~22 % full (fewer than 4 bits per x).  Measured at k = 1
-  // (DESIGN.md §3): 2^22..2^29 bits give 172.8, 156.8, 144.7, 137.0, 132.7, 130.3, 128.5, 128.1 ms.
+  uint32_t gate_log2 = 0, gate_probes = 0;
+  // Gate size for a geometry: 2^KHB_GATE_SPARSITY (default 64) bits per L1 x rounded up to a
+  // power of two, at most 2^30 bits (128 MiB) or 2^KHB_GATE_LOG2 from the environment (0
+  // disables); 0 when the map would be more than ~22 % full (fewer than 4 bits per x).  Probes:
+  // KHB_GATE_PROBES (default 3).  k = 1: 2^28 bits, 3 bits per x in one 64-bit block.
   static uint32_t gate_log2_for(const Geometry& g);
+  static uint32_t gate_probes_for();
   std::vector<Pt> lane_offs;             // offs[m] = (m*gpl) * _2GSn
 
   // progress(done, total) is called from the builder threads' coordinator.  `have` marks tables

@@ -236,7 +236,7 @@ int Session::open(const Tables& T, const SearchConfig& cfg, std::string& err) {
     khb_ctx* c = nullptr;
     int rc = khb_open(d, cfg.lanes, &c);
     if (!rc) rc = khb_load_bloom(c, bf.data(), T.l1[0].bytes, T.l1[0].bits, T.l1[0].hashes);
-    if (!rc && T.gate_log2 && cfg.use_gate) rc = khb_load_gate(c, T.gate.data(), T.gate_log2);
+    if (!rc && T.gate_log2 && cfg.use_gate) rc = khb_load_gate(c, T.gate.data(), T.gate_log2, T.gate_probes);
     if (!rc) rc = khb_load_giant_table(c, gsn.data());
     if (!rc) rc = khb_load_lane_offsets(c, offs.data(), (uint32_t)T.lane_offs.size(), T.gpl);
     if (rc) {

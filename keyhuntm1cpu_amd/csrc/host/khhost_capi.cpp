@@ -126,6 +126,8 @@ uint32_t khh_lane_offsets(const khh_tables* t, uint8_t* out, uint32_t* gpl) {
   return (uint32_t)t->t.lane_offs.size();
 }
 
+uint32_t khh_gate_probes(const khh_tables* t) { return t->t.gate_probes; }
+
 const uint8_t* khh_gate(const khh_tables* t, uint32_t* log2) {
   if (log2) *log2 = t->t.gate_log2;
   return t->t.gate_log2 ? t->t.gate.data() : nullptr;

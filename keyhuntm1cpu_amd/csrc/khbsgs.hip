@@ -46,6 +46,9 @@ struct AffPt {
 #ifndef KHB_LDSCOUNT
 #define KHB_LDSCOUNT 1            // probe-queue count through an LDS-typed pointer (ds_* not flat_*)
 #endif
+#ifndef KHB_NT
+#define KHB_NT 0                  // prefix scratch through non-temporal loads/stores
+#endif
 #ifndef KHB_FUSE
 #define KHB_FUSE 1                // -m bsgs walk: x = s^2 + nu fused into the squaring's reduction
 #endif
@@ -67,7 +70,9 @@ enum : int {
   kAddrB = 4,      // -m address, -l both (the reference default, keyhunt.cpp:300)
   kAddrDump = 5,   // -m address parity: write every x||y
   kBaby = 6,       // baby-step table build: bloom_add of every x into L1/L2/L3 + bPtable records
+  kScanG = 7,      // -m bsgs with a level-0 gate (the product path: walk_group_g)
 };
+constexpr bool is_scan(int m) { return m == kScan || m == kScanG; }
 constexpr bool is_addr(int m) { return m >= kAddrU && m <= kAddrDump; }
 constexpr bool needs_y(int m) { return m == kAddrU || m == kAddrB || m == kAddrDump; }
 constexpr bool is_dump(int m) { return m == kDump || m == kAddrDump || m == kBaby; }
@@ -75,6 +80,29 @@ constexpr uint32_t kHalf = KHB_GROUP / 2;            // 512
 constexpr uint32_t kCandCap = 1u << 20;
 constexpr uint32_t kAddrHitCap = 1u << 18;
 constexpr uint32_t kDegenCap = 4096;
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+// Prefix-scratch stream (written once by the forward pass, read once by the walk): with
+// KHB_NT the accesses are non-temporal, so the stream does not evict the level-0 gate from L2.
+__device__ __forceinline__ void scr_st(Fe* p, const Fe& v) {
+#if KHB_NT
+  v4u* q = reinterpret_cast<v4u*>(p);
+  __builtin_nontemporal_store(v4u{v.v[0], v.v[1], v.v[2], v.v[3]}, q);
+  __builtin_nontemporal_store(v4u{v.v[4], v.v[5], v.v[6], v.v[7]}, q + 1);
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ Fe scr_ld(const Fe* p) {
+#if KHB_NT
+  const v4u* q = reinterpret_cast<const v4u*>(p);
+  const v4u a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1);
+  return Fe{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
+#else
+  return *p;
+#endif
+}
 
 struct ScanArgs {
   const uint8_t* __restrict__ bloom;
@@ -96,12 +124,14 @@ struct ScanArgs {
   uint64_t bwords[3];
   uint64_t blimit[3];                  // ic < blimit[l] goes into level l (l1ext, m2, m3)
   uint32_t* __restrict__ bp;           // m3 x 16-byte struct bsgs_xvalue records (null = skipped)
-  // level-0 gate (khb_load_gate): bit (x & gate_mask) of a (gate_mask + 1)-bit map, set for every
-  // x of the L1 set; null = no gate.  kBaby writes it (gate_w, ic < glimit).
+  // level-0 gate (khb_load_gate): a blocked bloom of (gate_mask + 1) 64-bit blocks; x selects
+  // block x.v[0] & gate_mask and bits (x.v[1] >> 6p) & 63, p < gate_probes, in it, all set for
+  // every x of the L1 set; null = no gate.  kBaby writes it (gate_w, ic < glimit).
   const uint8_t* __restrict__ gate;
   uint32_t* __restrict__ gate_w;
+  uint32_t gate_probes;
   uint64_t glimit;
-  uint32_t gate_mask;
+  uint32_t gate_mask;                  // blocks - 1
   uint64_t job_keys;                   // baby steps per job
   uint64_t n_items;
   uint32_t n_jobs, group_begin, group_end, gpl, lanes_per_job, stride, cand_cap, degen_cap;
@@ -127,7 +157,7 @@ __device__ __forceinline__ void emit_cand(const ScanArgs& A, uint32_t job, uint3
 // bsgs_secondcheck would reject.
 constexpr uint32_t kDrainAt = 64;          // drain threshold (entries): one per lane
 constexpr uint32_t kQCap = kDrainAt + 64;           // entries per wave: < kDrainAt resident + <= 64 pushed
-constexpr uint32_t kQWords = 12;           // x[8], a lo, a hi, job, step index (SoA in LDS)
+constexpr uint32_t kQWords = 10;           // x[8], job, step index (SoA in LDS)
 constexpr uint32_t kWavesPerBlock = kBlock / 64;
 
 // The count lives in LDS, not in a register: lanes of a wave may diverge (the ragged last lane of
@@ -148,14 +178,12 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// Read queued entry k (x, a, job, step).
-__device__ __forceinline__ void q_read(const ProbeQueue& Q, uint32_t k, Fe& x, uint64_t& a, uint32_t& job,
-                                       uint32_t& step) {
+// Read queued entry k (x, job, step).
+__device__ __forceinline__ void q_read(const ProbeQueue& Q, uint32_t k, Fe& x, uint32_t& job, uint32_t& step) {
 #pragma unroll
   for (int d = 0; d < 8; ++d) x.v[d] = Q.q[d * kQCap + k];
-  a = (uint64_t)Q.q[8 * kQCap + k] | ((uint64_t)Q.q[9 * kQCap + k] << 32);
-  job = Q.q[10 * kQCap + k];
-  step = Q.q[11 * kQCap + k];
+  job = Q.q[8 * kQCap + k];
+  step = Q.q[9 * kQCap + k];
 }
 
 // Finish the newest min(n, active lanes) queued entries, one per lane, while n >= threshold.
@@ -170,44 +198,85 @@ __device__ __forceinline__ void q_drain(const ScanArgs& A, ProbeQueue& Q, uint32
     asm volatile("" ::: "memory");
     if (r < take) {
       Fe x;
-      uint64_t a;
       uint32_t job, step;
-      q_read(Q, n - take + r, x, a, job, step);
-      if (A.gate) fm_canon(x, x);       // gated pushes hold lazy x (scan_group's x_out)
+      q_read(Q, n - take + r, x, job, step);
+      fm_canon(x, x);                   // gated pushes hold lazy x (x_out)
       uint64_t w[4];
       x_words(w, x);
-      const uint8_t* bf = sub_bloom(A.bloom, A.geom, x);
-      if (A.gate ? bloom_full<KHB_PROBE_BITS>(bf, A.geom, w, xxh64_32(w, KHB_BLOOM_SEED))
-                 : bloom_rest_r<KHB_PROBE_BITS>(bf, A.geom, w, a))
+      // the whole level-1 check (bit 0 again for ungated pushes: the first hash is not queued)
+      if (bloom_full<KHB_PROBE_BITS>(sub_bloom(A.bloom, A.geom, x), A.geom, w, xxh64_32(w, KHB_BLOOM_SEED)))
         emit_cand(A, job, step);
     }
     asm volatile("" ::: "memory");
   }
 }
 
-// Queue x if its first bloom bit (hash a) is set.
-__device__ __forceinline__ void q_push(ProbeQueue& Q, bool hit, const Fe& x, uint64_t a, uint32_t job,
-                                       uint32_t step) {
+// Queue x if its first bit (L1 bit 0, or the gate bit) is set.
+__device__ __forceinline__ void q_push(ProbeQueue& Q, bool hit, const Fe& x, uint32_t job, uint32_t step) {
   const uint64_t m = __ballot(hit);
   const uint32_t n = *Q.n;
   if (hit) {
     const uint32_t k = n + lane_rank(m);
 #pragma unroll
     for (int d = 0; d < 8; ++d) Q.q[d * kQCap + k] = x.v[d];
-    Q.q[8 * kQCap + k] = (uint32_t)a;
-    Q.q[9 * kQCap + k] = (uint32_t)(a >> 32);
-    Q.q[10 * kQCap + k] = job;
-    Q.q[11 * kQCap + k] = step;
+    Q.q[8 * kQCap + k] = job;
+    Q.q[9 * kQCap + k] = step;
   }
   asm volatile("" ::: "memory");
   *Q.n = n + (uint32_t)__popcll(m);
 }
 
-// Gate bit (x & gate_mask), or without a gate L1 bit 0 (a = the first XXH64, queued with x).
+// The gate's bit positions in x's block: (x.v[1] >> 6p) & 63 for p < probes, packed 6 bits each
+// into three slots (unused probes repeat the last used one, so every test checks three bits).
+__device__ __forceinline__ uint32_t gate_bits(const ScanArgs& A, const Fe& x) {
+  const uint32_t w = x.v[1];
+  const uint32_t b0 = w & 63u, b1 = A.gate_probes > 1 ? (w >> 6) & 63u : b0;
+  const uint32_t b2 = A.gate_probes > 2 ? (w >> 12) & 63u : b1;
+  return b0 | (b1 << 6) | (b2 << 12);
+}
+
+// All three packed bits set in the 64-bit block (lo, hi)?
+__device__ __forceinline__ bool gate_block_pass(uint32_t lo, uint32_t hi, uint32_t bits) {
+  uint32_t r = 1u;
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    const uint32_t b = (bits >> (6 * p)) & 63u;
+    r &= ((b & 32u) ? hi : lo) >> (b & 31u);
+  }
+  return r & 1u;
+}
+
+// A gate test: x's 64-bit block of the map (one 8-byte load: a single cache line per x whatever
+// the probe count) and the packed bit positions.
+struct GatePend {
+  uint32_t lo, hi, bits;
+  __device__ __forceinline__ bool pass() const { return gate_block_pass(lo, hi, bits); }
+};
+
+__device__ __forceinline__ GatePend gate_issue(const ScanArgs& A, const Fe& x) {
+  const uint2 w = reinterpret_cast<const uint2*>(A.gate)[x.v[0] & A.gate_mask];
+  return GatePend{w.x, w.y, gate_bits(A, x)};
+}
+
+// kScanG: gate test of one walk step's two x (x2 absent at step 511: has2 = false, uniform).  Both
+// blocks are loaded before either is waited for; survivors (~0.04 % of x) go to the queue.
+__device__ __forceinline__ void gate_pair(const ScanArgs& A, ProbeQueue& Q, const Fe& x1, uint32_t step1, bool has2,
+                                          const Fe& x2, uint32_t step2, uint32_t job) {
+  const GatePend q1 = gate_issue(A, x1), q2 = gate_issue(A, x2);
+  const bool h1 = q1.pass(), h2 = has2 && q2.pass();
+  if (__ballot(h1 || h2) == 0) return;
+  q_push(Q, h1, x1, job, step1);
+  q_drain(A, Q, kDrainAt);
+  q_push(Q, h2, x2, job, step2);
+  q_drain(A, Q, kDrainAt);
+}
+
+// Gate bits of x (blocked gate), or without a gate L1 bit 0 (a = the first XXH64).
 __device__ __forceinline__ bool first_bit(const ScanArgs& A, const Fe& x, uint64_t& a) {
   if (A.gate) {
     a = 0;
-    return test_bit(A.gate, x.v[0] & A.gate_mask);
+    const uint2 w = reinterpret_cast<const uint2*>(A.gate)[x.v[0] & A.gate_mask];
+    return gate_block_pass(w.x, w.y, gate_bits(A, x));
   }
   uint64_t w[4];
   x_words(w, x);
@@ -225,7 +294,7 @@ __device__ __forceinline__ void probe(const ScanArgs& A, ProbeQueue& Q, const Fe
 #if KHB_PROBE_MODE == 0
     uint64_t a;
     const bool hit = first_bit(A, x, a);
-    q_push(Q, hit, x, a, job, j * KHB_GROUP + t);
+    q_push(Q, hit, x, job, j * KHB_GROUP + t);
     q_drain(A, Q, kDrainAt);
 #elif KHB_PROBE_MODE == 1      // perf experiment: first hash only, no bloom access
     uint64_t w[4];
@@ -266,9 +335,9 @@ __device__ __forceinline__ void probe_pair(const ScanArgs& A, ProbeQueue& Q, con
     uint64_t a1, a2;
     const bool h1 = first_bit(A, x1, a1);
     const bool h2 = first_bit(A, x2, a2);
-    q_push(Q, h1, x1, a1, job, j * KHB_GROUP + t1);
+    q_push(Q, h1, x1, job, j * KHB_GROUP + t1);
     q_drain(A, Q, kDrainAt);
-    q_push(Q, h2, x2, a2, job, j * KHB_GROUP + t2);
+    q_push(Q, h2, x2, job, j * KHB_GROUP + t2);
     q_drain(A, Q, kDrainAt);
     return;
   }
@@ -361,8 +430,11 @@ __device__ __forceinline__ void baby_point(const ScanArgs& A, const Fe& x, uint3
   x_words(w, x);
   const uint64_t a = xxh64_32(w, KHB_BLOOM_SEED);
   if (A.gate_w && ic < A.glimit) {
-    const uint32_t gb = x.v[0] & A.gate_mask;
-    atomicOr(A.gate_w + (gb >> 5), 1u << (gb & 31));
+    const uint32_t blk = x.v[0] & A.gate_mask;
+    for (uint32_t p = 0; p < A.gate_probes; ++p) {
+      const uint32_t b = (x.v[1] >> (6 * p)) & 63u;
+      atomicOr(A.gate_w + 2 * blk + (b >> 5), 1u << (b & 31));
+    }
   }
   const uint64_t b = xxh64_32(w, a);
   const uint32_t sub = x.v[7] >> 24;
@@ -385,7 +457,7 @@ __device__ __forceinline__ void baby_point(const ScanArgs& A, const Fe& x, uint3
 // per wave), and the drain canonicalises its survivors before hashing.
 template <int MODE>
 __device__ __forceinline__ void x_out(const ScanArgs& A, Fe& x) {
-  if (MODE == kScan && A.gate) {
+  if ((MODE == kScan && A.gate) || MODE == kScanG) {
     if (x.v[7] == 0xffffffffu) fm_canon(x, x);
   } else {
     fm_canon(x, x);
@@ -406,9 +478,10 @@ __device__ __forceinline__ void walk_group(const ScanArgs& A, ProbeQueue& Q, con
   Fe pre, dx;
   // KHB_PIPE bit 0: the prefix for step i-1 is loaded during step i, so its HBM latency hides
   // behind a whole step's arithmetic instead of being waited for right after the load.
-  constexpr bool PREFETCH = (KHB_PIPE & 1) && MODE == kScan;
-  Fe pre_next;
-  if (PREFETCH) pre_next = scr[(size_t)(kHalf - 2) * S];
+  constexpr bool PREFETCH = (KHB_PIPE & 1) && is_scan(MODE);
+  // The load goes into `pre` itself right after its last use (no loop-carried copy: a copy at the
+  // loop latch would make the wave wait for the load there).
+  if (PREFETCH) pre = scr[(size_t)(kHalf - 2) * S];
   // KHB_FUSE (-m bsgs x-only walks): C.x is carried as negCx = p - C.x, so dx = GSn.x + negCx and
   // x = s^2 + (negCx - GSn.x) need no separate modular subtraction of the centre.
   constexpr bool FUSED = KHB_FUSE && (MODE == kScan || MODE == kDump);
@@ -422,13 +495,9 @@ __device__ __forceinline__ void walk_group(const ScanArgs& A, ProbeQueue& Q, con
   for (int i = (int)kHalf - 1; i >= 0; --i) {
     Fe idx;
     if (i > 0) {
-      if (PREFETCH) {
-        pre = pre_next;
-        if (i > 1) pre_next = scr[(size_t)(i - 2) * S];
-      } else {
-        pre = scr[(size_t)(i - 1) * S];
-      }
+      if (!PREFETCH) pre = scr[(size_t)(i - 1) * S];
       fm_mul(idx, inv, pre);
+      if (PREFETCH && i > 1) pre = scr[(size_t)(i - 2) * S];
       const Fe gx = gsn.x(i);
       if constexpr (FUSED) fm_add_lazy(dx, gx, negCx); else fm_sub(dx, gx, C.x);
       fm_mul(inv, inv, dx);
@@ -451,7 +520,7 @@ __device__ __forceinline__ void walk_group(const ScanArgs& A, ProbeQueue& Q, con
         fm_mul(s, s, idx);
         fm_sqr_add(x2, s, u);
         x_out<MODE>(A, x2);
-        if constexpr ((KHB_PIPE & 2) && MODE == kScan)
+        if constexpr ((KHB_PIPE & 2) && is_scan(MODE))
           asm volatile("" ::"v"(x1.v[0]), "v"(x2.v[0]), "v"(x1.v[7]), "v"(x2.v[7]) : "memory");
         probe_pair<DUMP>(A, Q, x1, x2, job, j, kHalf - 1 - (uint32_t)i, kHalf + 1 + (uint32_t)i);
       } else {
@@ -514,6 +583,65 @@ __device__ __forceinline__ void walk_group(const ScanArgs& A, ProbeQueue& Q, con
     addr_point<MODE>(A, C.x, C.y, job, j, kHalf);
   else
     probe<DUMP>(A, Q, C.x, job, j, kHalf);
+}
+
+// walk_group for kScanG (-m bsgs with a level-0 gate), the product path: same points, same order,
+// with the fused x-only arithmetic (x = s^2 + nu, KHB_FUSE), the prefix of step i-1 loaded right
+// after step i's last use of the prefix register (its HBM latency hides behind a whole step), and
+// each step's two x gate-tested together (gate_pair).  The first step is peeled and the prefix
+// load is unconditional, so the loop body issues the same vector-memory sequence every time and
+// the waitcnt pass waits for exactly the operand it needs.
+__device__ __forceinline__ void walk_group_g(const ScanArgs& A, ProbeQueue& Q, const AffPt& C, Fe inv,
+                                             uint32_t job, uint32_t j, const Fe* scr) {
+  const size_t S = A.stride;
+  const GsnTable gsn{A.gsn};
+  const uint32_t base = j * KHB_GROUP;
+  Fe negCx;
+  {
+    Fe p;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p.v[k] = k == 0 ? KHB_P0 : (k == 1 ? KHB_P1 : 0xFFFFFFFFu);
+    fm_sub(negCx, p, C.x);
+  }
+  Fe pre = scr_ld(scr + (size_t)(kHalf - 2) * S);
+  Fe idx, dx, u, s, x1, x2;
+  // step 511: pts[0] = C - GSn[511] only
+  {
+    fm_mul(idx, inv, pre);
+    pre = scr_ld(scr + (size_t)(kHalf - 3) * S);
+    fm_add_lazy(dx, gsn.x(kHalf - 1), negCx);
+    fm_mul(inv, inv, dx);
+    const AffPt g = gsn.pt(kHalf - 1);
+    fm_sub(u, negCx, g.x);
+    fm_add_lazy(s, g.y, C.y);
+    fm_mul(s, s, idx);
+    fm_sqr_add(x1, s, u);
+    x_out<kScanG>(A, x1);
+    gate_pair(A, Q, x1, base, false, x1, 0, job);
+  }
+  for (int i = (int)kHalf - 2; i >= 0; --i) {
+    if (i > 0) {
+      fm_mul(idx, inv, pre);
+      pre = scr_ld(scr + (size_t)(i >= 2 ? i - 2 : 0) * S);   // i = 1: a harmless reload of prefix 0
+      fm_add_lazy(dx, gsn.x(i), negCx);
+      fm_mul(inv, inv, dx);
+    } else {
+      idx = inv;
+    }
+    const AffPt g = gsn.pt(i);
+    fm_sub(u, negCx, g.x);
+    // C - GSn[i] (pts[511 - i]) and C + GSn[i] (pts[513 + i])
+    fm_add_lazy(s, g.y, C.y);
+    fm_mul(s, s, idx);
+    fm_sqr_add(x1, s, u);
+    x_out<kScanG>(A, x1);
+    fm_sub(s, g.y, C.y);
+    fm_mul(s, s, idx);
+    fm_sqr_add(x2, s, u);
+    x_out<kScanG>(A, x2);
+    gate_pair(A, Q, x1, base + kHalf - 1 - (uint32_t)i, true, x2, base + kHalf + 1 + (uint32_t)i, job);
+  }
+  probe<false>(A, Q, C.x, job, j, kHalf);        // the centre, pts[512]
 }
 
 // One reference group centred on C, walked on its own (-m address, baby steps): the 513-element
@@ -705,11 +833,11 @@ __device__ __forceinline__ void scan_batch(const ScanArgs& A, ProbeQueue& Q, uin
     const Fe cx = sc[2 * g * S];
     Fe a, dx;
     fm_sub(a, gsn.x(0), cx);
-    sg[0] = a;
+    scr_st(sg, a);
     for (uint32_t i = 1; i < kHalf - 1; ++i) {
       fm_sub(dx, gsn.x(i), cx);
       fm_mul(a, a, dx);
-      sg[i * S] = a;
+      scr_st(sg + i * S, a);
     }
     fm_sub(dx, gsn.x(kHalf - 1), cx);
     fm_mul(a, a, dx);
@@ -742,7 +870,10 @@ __device__ __forceinline__ void scan_batch(const ScanArgs& A, ProbeQueue& Q, uin
     Fe* const sg = scr + (size_t)g * kHalf * S;
     asm volatile("" ::: "memory");
     const AffPt C{sc[2 * g * S], sc[(2 * g + 1) * S]};
-    walk_group<MODE>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
+    if constexpr (MODE == kScanG)
+      walk_group_g(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
+    else
+      walk_group<MODE>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
     if (MODE != kDump && ((degen >> g) & 1u)) {
       const uint32_t k = atomicAdd(&A.counters[1], 1u);
       if (k < A.degen_cap) A.degen[k] = khb_degenerate{job, g0 + g};
@@ -793,8 +924,8 @@ __global__ void k_expand_offsets(const AffPt* __restrict__ offs, uint32_t gpl, c
 
 template <int MODE>
 __global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanArgs A) {
-  constexpr bool QUEUE = MODE == kScan;
-  constexpr bool BATCH = MODE == kScan || MODE == kDump;
+  constexpr bool QUEUE = is_scan(MODE);
+  constexpr bool BATCH = is_scan(MODE) || MODE == kDump;
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   Fe* scr = A.scratch + lane;
   __shared__ uint32_t s_queue[QUEUE ? kWavesPerBlock : 1][QUEUE ? kQWords * kQCap : 1];
@@ -886,7 +1017,7 @@ struct khb_ctx {
   uint8_t* d_bloom = nullptr;
   BloomGeom geom{};
   uint8_t* d_gate = nullptr;           // level-0 gate (khb_load_gate), null = none
-  uint32_t gate_mask = 0;
+  uint32_t gate_mask = 0, gate_probes = 0;
   AffPt* d_gsn = nullptr;
   AffPt* d_offs = nullptr;
   uint32_t n_offs = 0, gpl = 0;
@@ -950,6 +1081,7 @@ ScanArgs make_args(khb_ctx* c, uint32_t n_jobs, uint32_t group_begin, uint32_t g
   A.geom = c->geom;
   A.gate = c->d_gate;
   A.gate_mask = c->gate_mask;
+  A.gate_probes = c->gate_probes;
   A.gsn = c->d_gsn;
   A.offs = c->d_offs;
   A.gofs = c->gpl == 1 ? c->d_offs : c->d_gofs;
@@ -1091,8 +1223,9 @@ int khb_close(khb_ctx* c) {
   return KHB_OK;
 }
 
-int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits) {
-  if (!c || (gate && (log2_bits < 13 || log2_bits > 32))) return KHB_EINVAL;
+int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t probes) {
+  if (!c || (gate && (log2_bits < 13 || log2_bits > 32 || probes < 1 || probes > KHB_GATE_MAX_PROBES)))
+    return KHB_EINVAL;
   if (c->in_flight) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
   if (c->d_gate) { hipFree(c->d_gate); c->d_gate = nullptr; }
@@ -1101,7 +1234,8 @@ int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits) {
   const size_t bytes = (size_t)1 << (log2_bits - 3);
   KHB_TRY(c, hipMalloc(&c->d_gate, bytes));
   KHB_TRY(c, hipMemcpy(c->d_gate, gate, bytes, hipMemcpyHostToDevice));
-  c->gate_mask = (uint32_t)((1ull << log2_bits) - 1);
+  c->gate_mask = (uint32_t)((1ull << (log2_bits - 6)) - 1);
+  c->gate_probes = probes;
   return KHB_OK;
 }
 
@@ -1165,7 +1299,10 @@ int khb_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t gro
   ScanArgs A = make_args(c, n_jobs, group_begin, group_count, kBatch);
   const uint32_t blocks = c->lanes / kBlock;
   KHB_TRY(c, hipEventRecord(c->ev0, c->stream));
-  hipLaunchKernelGGL(k_giant_scan<kScan>, dim3(blocks), dim3(kBlock), 0, c->stream, A);
+  if (c->d_gate)
+    hipLaunchKernelGGL(k_giant_scan<kScanG>, dim3(blocks), dim3(kBlock), 0, c->stream, A);
+  else
+    hipLaunchKernelGGL(k_giant_scan<kScan>, dim3(blocks), dim3(kBlock), 0, c->stream, A);
   KHB_TRY(c, hipGetLastError());
   KHB_TRY(c, hipEventRecord(c->ev1, c->stream));
   KHB_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, 16, hipMemcpyDeviceToHost, c->stream));
@@ -1421,11 +1558,12 @@ int khb_hash160(khb_ctx* c, int kind, const uint8_t* xy, uint8_t* out, uint32_t 
 int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t groups_per_job, uint64_t l1ext,
                    uint64_t m2, uint64_t m3, const uint64_t bytes_per_sub[3], const uint64_t bits_per_sub[3],
                    const uint32_t hashes[3], uint8_t* l1, uint8_t* l2, uint8_t* l3, uint8_t* bp, uint8_t* gate,
-                   uint32_t gate_log2, float* kernel_ms) {
+                   uint32_t gate_log2, uint32_t gate_probes, float* kernel_ms) {
   int rc = check_scan_args(c, centres, n_jobs, 0, groups_per_job, false);
   if (rc) return rc;
   if (!bytes_per_sub || !bits_per_sub || !hashes) return KHB_EINVAL;
-  if (gate && (gate_log2 < 13 || gate_log2 > 32)) return KHB_EINVAL;
+  if (gate && (gate_log2 < 13 || gate_log2 > 32 || gate_probes < 1 || gate_probes > KHB_GATE_MAX_PROBES))
+    return KHB_EINVAL;
   uint8_t* outs[3] = {l1, l2, l3};
   for (int l = 0; l < 3; ++l)
     if (outs[l] && (bits_per_sub[l] < 2 || (bits_per_sub[l] + 7) / 8 != bytes_per_sub[l] || hashes[l] == 0 ||
@@ -1450,7 +1588,8 @@ int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t
     if (e == hipSuccess) e = hipMemsetAsync(dgate, 0, gate_bytes, c->stream);
     A.gate_w = dgate;
     A.glimit = l1ext;
-    A.gate_mask = (uint32_t)((1ull << gate_log2) - 1);
+    A.gate_mask = (uint32_t)((1ull << (gate_log2 - 6)) - 1);
+    A.gate_probes = gate_probes;
   }
   for (int l = 0; l < 3 && e == hipSuccess; ++l) {
     if (!outs[l]) continue;

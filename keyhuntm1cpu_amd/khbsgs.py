@@ -63,7 +63,7 @@ def lib(path: str | None = None) -> C.CDLL:
         L.khb_groups_per_item.argtypes = []
         L.khb_load_bloom.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, C.c_uint64, C.c_uint32]
         L.khb_load_giant_table.argtypes = [C.c_void_p, C.c_char_p]
-        L.khb_load_gate.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32]
+        L.khb_load_gate.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32]
         L.khb_load_lane_offsets.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32]
         L.khb_submit.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]
         L.khb_collect.argtypes = [C.c_void_p, P(Cand), C.c_uint32, P(Degenerate), C.c_uint32, P(Stats)]
@@ -138,11 +138,11 @@ class Engine:
         assert len(bf) == 256 * bytes_per_sub
         _check(self.L.khb_load_bloom(self.h, bf, bytes_per_sub, bits, hashes), self.h, self.L)
 
-    def load_gate(self, gate: bytes | None, log2_bits: int = 0) -> None:
-        """Level-0 gate in front of the L1 probe (None removes it)."""
+    def load_gate(self, gate: bytes | None, log2_bits: int = 0, probes: int = 1) -> None:
+        """Level-0 gate in front of the L1 probe (None removes it); probes = bits per x."""
         if gate is not None:
             assert len(gate) == (1 << log2_bits) // 8
-        _check(self.L.khb_load_gate(self.h, gate, log2_bits if gate is not None else 0), self.h, self.L)
+        _check(self.L.khb_load_gate(self.h, gate, log2_bits if gate is not None else 0, probes), self.h, self.L)
 
     def load_giant_table(self, gsn: bytes) -> None:
         assert len(gsn) == 513 * 64

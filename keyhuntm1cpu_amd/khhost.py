@@ -44,6 +44,8 @@ def lib() -> C.CDLL:
         L.khh_bptable.argtypes = [C.c_void_p, P(C.c_uint64)]
         L.khh_gate.restype = C.c_void_p
         L.khh_gate.argtypes = [C.c_void_p, P(C.c_uint32)]
+        L.khh_gate_probes.restype = C.c_uint32
+        L.khh_gate_probes.argtypes = [C.c_void_p]
         L.khh_chunk_centre.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p]
         L.khh_secondcheck.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_char_p, C.c_char_p]
         L.khh_search.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, P(C.c_int), C.c_int,
@@ -168,6 +170,10 @@ class Tables:
         b = C.create_string_buffer(64 * n)
         lib().khh_lane_offsets(self.h, b, C.byref(g))
         return b.raw, int(g.value)
+
+    def gate_probes(self) -> int:
+        """Bits per x of the level-0 gate (khb_load_gate's probes); 0 when there is no gate."""
+        return int(lib().khh_gate_probes(self.h))
 
     def gate(self) -> tuple[bytes, int]:
         """The level-0 gate (khb_load_gate) and its log2 size; (b"", 0) when the tables have none."""

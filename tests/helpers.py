@@ -29,3 +29,15 @@ def rand_fe(rng: random.Random) -> int:
     if r < 0.2:
         return rng.randrange(1 << 64)
     return rng.randrange(P)
+
+
+def gate_bits(lg: int, probes: int, x: int) -> list[int]:
+    """Bit indices of the level-0 gate (khb_load_gate) for x: a blocked bloom of 64-bit blocks,
+    block (x mod 2^32) mod 2^(lg-6), bits ((x >> 32) mod 2^32 >> 6p) mod 64 within it, p < probes."""
+    blk = (x & 0xFFFFFFFF) & ((1 << (lg - 6)) - 1)
+    w1 = (x >> 32) & 0xFFFFFFFF
+    return [64 * blk + ((w1 >> (6 * p)) & 63) for p in range(probes)]
+
+
+def gate_pass(gate: bytes, lg: int, probes: int, x: int) -> bool:
+    return all((gate[b >> 3] >> (b & 7)) & 1 for b in gate_bits(lg, probes, x))

@@ -8,7 +8,7 @@ import random
 
 import pytest
 
-from tests.helpers import P, lane_offsets, rand_fe
+from tests.helpers import P, gate_pass, lane_offsets, rand_fe
 
 pytestmark = pytest.mark.gpu
 
@@ -196,11 +196,14 @@ def _l1_check(bf: bytes, nb: int, bits: int, hashes: int, xb: bytes, ora) -> boo
     return True
 
 
-def test_gate_candidates_exact(eng, bs32, ora):
+@pytest.mark.parametrize("probes", [1, 3])
+def test_gate_candidates_exact(eng, bs32, ora, probes):
     """Level-0 gate (khb_load_gate): the candidates are exactly the giant steps whose x passes the
-    level-1 bloom AND whose gate bit x mod 2^log2 is set.  A dense synthetic L1 (each bit
-    set with p = 0.97, so ~54 % of all x pass) and a random half-full gate exercise both paths on
-    every x of four chunks; without the gate the same scan returns the plain L1 candidates."""
+    level-1 bloom AND whose gate bits (helpers.gate_bits: one 64-bit block, `probes` bits in it)
+    are all set.  A dense synthetic L1 (each bit set with p = 0.97, so ~54 % of all x pass) and a
+    random gate (each bit set with p = 0.5^(1/probes), so about half of all x pass it) exercise
+    both paths on every x of four chunks; without the gate the same scan returns the plain L1
+    candidates."""
     gpl = 4
     load_tables(eng, bs32, gpl)
     _, nb, bits, hashes = bs32.bloom_concat(1)
@@ -208,7 +211,8 @@ def test_gate_candidates_exact(eng, bs32, ora):
     bf = bytes(sum(1 << k for k in range(8) if rng.random() < 0.97) for _ in range(256 * nb))
     eng.load_bloom(bf, nb, bits, hashes)
     lg = 16
-    gate = bytes(rng.getrandbits(8) for _ in range((1 << lg) // 8))
+    fill = 0.5 ** (1.0 / probes)
+    gate = bytes(sum(1 << k for k in range(8) if rng.random() < fill) for _ in range((1 << lg) // 8))
     centres, l1_ref, gate_ref = [], [], []
     for c in range(4):
         st = bs32.chunk_start(0x3000000000000000 + c * (1 << 33), ora.pubkey(0xABCDEF0123 + c))
@@ -219,14 +223,13 @@ def test_gate_candidates_exact(eng, bs32, ora):
             xb = xs[32 * a:32 * a + 32]
             if _l1_check(bf, nb, bits, hashes, xb, ora):
                 l1.append(a)
-                g = int.from_bytes(xb, "big") & ((1 << lg) - 1)
-                if (gate[g >> 3] >> (g & 7)) & 1:
+                if gate_pass(gate, lg, probes, int.from_bytes(xb, "big")):
                     gt.append(a)
         l1_ref.append(l1)
         gate_ref.append(gt)
     try:
         for use_gate, ref in ((False, l1_ref), (True, gate_ref)):
-            eng.load_gate(gate if use_gate else None, lg)
+            eng.load_gate(gate if use_gate else None, lg, probes)
             got, degen, _ = eng.scan(b"".join(centres), 0, bs32.cycles)
             per_job = [[] for _ in centres]
             for job, a in got:

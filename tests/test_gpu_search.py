@@ -9,6 +9,7 @@ import subprocess
 import pytest
 
 from keyhuntm1cpu_amd import BIN_DIR, khhost
+from tests.helpers import gate_pass
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -85,12 +86,13 @@ def test_full_geometry_candidates_match_oracle(tables_k1, ora):
 
 
 def test_full_geometry_gate(tables_k1, ora):
-    """The product's level-0 gate on the real k=1 tables (2^25 bits): over two whole chunks the gated
-    candidates are exactly the L1 candidates whose gate bit is set (x from the GPU dump of their
-    group), and the key's hit survives the gate."""
+    """The product's level-0 gate on the real k=1 tables (2^28 bits, three bits per x in one 64-bit
+    block): over two whole chunks the gated candidates are exactly the L1 candidates whose gate
+    bits are set (x from the GPU dump of their group), and the key's hit survives the gate."""
     from keyhuntm1cpu_amd.khbsgs import Engine
     gate, lg = tables_k1.gate()
-    assert lg == 28
+    probes = tables_k1.gate_probes()
+    assert lg == 28 and probes == 3
     key = 0x2832ED74F2B5E35EE
     t = ora.pubkey(key)
     bases = [key - 123456789012, (1 << 65) + (5 << 45)]
@@ -102,15 +104,14 @@ def test_full_geometry_gate(tables_k1, ora):
         e.load_lane_offsets(offs, gpl)
         centres = [tables_k1.chunk_centre(b, t.be64()) for b in bases]
         plain, _, _ = e.scan(b"".join(centres), 0, tables_k1.cycles)
-        e.load_gate(gate, lg)
+        e.load_gate(gate, lg, probes)
         gated, _, st = e.scan(b"".join(centres), 0, tables_k1.cycles)
         exp = []
         for j, a in plain:
             g0 = (a // 1024) // gpl * gpl
             xs = e.dump_x(centres[j], g0, gpl)
             xb = xs[32 * (a - g0 * 1024):32 * (a - g0 * 1024) + 32]
-            gb = int.from_bytes(xb, "big") & ((1 << lg) - 1)
-            if (gate[gb >> 3] >> (gb & 7)) & 1:
+            if gate_pass(gate, lg, probes, int.from_bytes(xb, "big")):
                 exp.append((j, a))
     assert sorted(gated) == sorted(exp)
     assert any(tables_k1.secondcheck(bases[0], a, t.be64()) == key for j, a in gated if j == 0)

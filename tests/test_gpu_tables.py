@@ -15,7 +15,7 @@ def _same(a, b):
     assert a.bptable() == b.bptable()
     assert a.giant_table() == b.giant_table()
     assert a.lane_offsets() == b.lane_offsets()
-    assert a.gate() == b.gate() and a.gate()[1] >= 13
+    assert a.gate() == b.gate() and a.gate()[1] >= 13 and a.gate_probes() == b.gate_probes() == 3
 
 
 @pytest.mark.parametrize("n,k", [("0x40000000", 33),      # M = 33*2^15: L1 extent overshoot (quirk vi)

@@ -10,6 +10,7 @@ import random
 import pytest
 
 from keyhuntm1cpu_amd import khhost
+from tests.helpers import gate_bits
 
 GEOMS = [("0x100000", 1), ("0x100000000", 1), ("0x100000000", 3), ("0x10000000000", 2)]
 
@@ -90,16 +91,18 @@ def test_pubkey_and_parse(ora):
 
 
 def test_level0_gate_exact(pair, ora):
-    """The level-0 gate (khb_load_gate) is exactly the set of bits x mod 2^log2 over the
-    baby steps of the L1 set (ic < l1ext, key ic + 1): every L1 member passes it, nothing else is set."""
+    """The level-0 gate (khb_load_gate, a blocked bloom: helpers.gate_bits) is exactly the set of the
+    bits of the baby steps of the L1 set (ic < l1ext, key ic + 1): every L1 member passes it,
+    nothing else is set."""
     h, o = pair
     if o.l1ext > 1 << 17:
         pytest.skip("baby set too large for the Python walk")
     gate, lg = h.gate()
-    assert lg >= 13 and len(gate) == (1 << lg) // 8
+    probes = h.gate_probes()
+    assert lg >= 13 and len(gate) == (1 << lg) // 8 and probes == 3
     exp = bytearray(len(gate))
     for ic in range(o.l1ext):
         x = ora.pubkey(ic + 1).xy()[0]
-        b = x & ((1 << lg) - 1)
-        exp[b >> 3] |= 1 << (b & 7)
+        for b in gate_bits(lg, probes, x):
+            exp[b >> 3] |= 1 << (b & 7)
     assert gate == bytes(exp)

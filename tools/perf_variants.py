@@ -3,8 +3,9 @@ Usage: python tools/perf_variants.py [lib.so ...]   (default: the product librar
 Tables: product host engine, default geometry (k=1, or K=...), puzzle #66 target, JOBS (256) chunks
 per launch.
 GATE=0|1|both (default both): run every library without / with the level-0 gate.
-GATE_LOG2S=23,24 adds gates of those sizes, folded from the tables' gate (bit i of a 2^(L-1) map is
-bit 2i | bit 2i+1 of the 2^L map: the same map a 2^(L-1) build writes)."""
+GATE_LOG2S=23,24 adds gates of those sizes, folded from the tables' gate (64-bit block i of a
+2^(L-1)-bit map is block i | block i + 2^(L-7) of the 2^L map: the same map a 2^(L-1) build writes,
+the block index being (x mod 2^32) mod 2^(L-6))."""
 import glob
 import os
 import statistics
@@ -31,8 +32,8 @@ gsets = [0, glog] if gmode == "both" else [glog if gmode == "1" else 0]
 gates = {glog: gate}
 import numpy as np  # noqa: E402
 for lg in [int(v) for v in os.environ.get("GATE_LOG2S", "").split(",") if v]:
-    bv = np.unpackbits(np.frombuffer(gate, np.uint8), bitorder="little")
-    gates[lg] = np.packbits(bv.reshape(-1, 1 << (glog - lg)).max(axis=1), bitorder="little").tobytes()
+    blocks = np.frombuffer(gate, np.uint64)
+    gates[lg] = np.bitwise_or.reduce(blocks.reshape(1 << (glog - lg), -1), axis=0).tobytes()
     gsets.append(lg)
 engines = {}
 for p in paths:
@@ -40,7 +41,7 @@ for p in paths:
         e = Engine(0, lib_path=p)
         e.load_bloom(bf, nb, bits, h)
         if g:
-            e.load_gate(gates[g], g)
+            e.load_gate(gates[g], g, t.gate_probes())
         e.load_giant_table(gsn)
         e.load_lane_offsets(offs, gpl)
         e.scan(centres[:64 * 8], 0, 64)
