@@ -26,6 +26,32 @@ namespace khb {
 
 #define FM_DEV __device__ __forceinline__
 
+// KHB_RARE: carry/borrow propagation past limb 1/2 that happens with probability ~2^-30 per call
+// (the fold of 2^256 = 0x1000003D1 into a random 256-bit value) runs behind a wave-uniform branch
+// taken only when some lane needs it; the common path stops the chain at the limb that produces
+// the carry.  The branch body is the full propagation, a no-op for lanes whose carry is 0.
+#ifndef KHB_RARE
+#define KHB_RARE 1
+#endif
+#if KHB_RARE_FORCE    // test builds: always take the rare branch (its full propagation is a no-op at c = 0)
+FM_DEV bool fm_any(uint32_t) { return true; }
+#else
+FM_DEV bool fm_any(uint32_t c) { return __builtin_expect(__ballot(c != 0) != 0, 0); }
+#endif
+
+// r[k..7] += c (c in {0, 1} per lane), carry-out returned.
+template <int K>
+FM_DEV uint32_t fm_propagate(uint32_t* r, uint32_t c) {
+  uint32_t co = c;
+#pragma unroll
+  for (int i = K; i < 8; ++i) {
+    const uint64_t t = (uint64_t)r[i] + co;
+    r[i] = (uint32_t)t;
+    co = (uint32_t)(t >> 32);
+  }
+  return co;
+}
+
 // acc += a*b ; c2 += carry-out
 FM_DEV void fm_madc(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
   asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
@@ -529,6 +555,33 @@ FM_DEV void fm_reduce_T(Fe& r, const uint32_t T[10], const uint32_t* H) {
   const uint64_t w = (uint64_t)(uint32_t)(u >> 32) + R8;                              // limb-1 addend
   const uint32_t w2 = (uint32_t)(w >> 32) + R9;                                       // limb-2 addend (<= 3)
   uint32_t c;
+#if KHB_RARE
+  // limbs 0..2 take the addends; the carry into limb 3 (probability ~2^-30) is propagated, and
+  // a wrap past 2^256 (~2^-212) folded, only in the rare branch.
+  uint32_t c3;
+  asm("v_add_co_u32_e32 %0, vcc, %0, %4\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %1, %5, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %2, %6, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %3, vcc, 0, %7, vcc"
+      : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "=&v"(c3)
+      : "v"((uint32_t)u), "v"((uint32_t)w), "v"(w2), "v"(0u)
+      : "vcc");
+  if (fm_any(c3)) {
+    c = fm_propagate<3>(R, c3);
+    const uint32_t k0 = c * 977u;
+    uint64_t t = (uint64_t)R[0] + k0;
+    R[0] = (uint32_t)t;
+    t = (uint64_t)R[1] + c + (t >> 32);
+    R[1] = (uint32_t)t;
+    fm_propagate<2>(R, (uint32_t)(t >> 32));
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = R[i];
+  return;
+#endif
   asm("v_add_co_u32_e32 %0, vcc, %0, %9\n\t"
       "s_nop 0\n\t"
       "v_addc_co_u32_e32 %1, vcc, %1, %10, vcc\n\t"
@@ -627,31 +680,35 @@ FM_DEV void fm_sqr_generic(Fe& r, const Fe& a) {
 
 // a - b mod p for a < 2^256, b < p.
 FM_DEV void fm_sub(Fe& r, const Fe& a, const Fe& b) {
-  uint32_t d[8], m, k0, k1;
-  asm("v_sub_co_u32_e32 %0, vcc, %11, %19\n\t"
+  uint32_t d[8], m, k0, k1, b2;
+  asm("v_sub_co_u32_e32 %0, vcc, %12, %20\n\t"
       "s_nop 0\n\t"
-      "v_subb_co_u32_e32 %1, vcc, %12, %20, vcc\n\t"
+      "v_subb_co_u32_e32 %1, vcc, %13, %21, vcc\n\t"
       "s_nop 0\n\t"
-      "v_subb_co_u32_e32 %2, vcc, %13, %21, vcc\n\t"
+      "v_subb_co_u32_e32 %2, vcc, %14, %22, vcc\n\t"
       "s_nop 0\n\t"
-      "v_subb_co_u32_e32 %3, vcc, %14, %22, vcc\n\t"
+      "v_subb_co_u32_e32 %3, vcc, %15, %23, vcc\n\t"
       "s_nop 0\n\t"
-      "v_subb_co_u32_e32 %4, vcc, %15, %23, vcc\n\t"
+      "v_subb_co_u32_e32 %4, vcc, %16, %24, vcc\n\t"
       "s_nop 0\n\t"
-      "v_subb_co_u32_e32 %5, vcc, %16, %24, vcc\n\t"
+      "v_subb_co_u32_e32 %5, vcc, %17, %25, vcc\n\t"
       "s_nop 0\n\t"
-      "v_subb_co_u32_e32 %6, vcc, %17, %25, vcc\n\t"
+      "v_subb_co_u32_e32 %6, vcc, %18, %26, vcc\n\t"
       "s_nop 0\n\t"
-      "v_subb_co_u32_e32 %7, vcc, %18, %26, vcc\n\t"
+      "v_subb_co_u32_e32 %7, vcc, %19, %27, vcc\n\t"
       // m = borrow ? 0xffffffff : 0 ; subtract (0x1000003D1 & m), i.e. add p on borrow
       "s_nop 0\n\t"
-      "v_subb_co_u32_e32 %8, vcc, 0, %27, vcc\n\t"
+      "v_subb_co_u32_e32 %8, vcc, 0, %28, vcc\n\t"
       "v_and_b32_e32 %9, 0x3d1, %8\n\t"
       "v_and_b32_e32 %10, 1, %8\n\t"
       "v_sub_co_u32_e32 %0, vcc, %0, %9\n\t"
       "s_nop 0\n\t"
       "v_subb_co_u32_e32 %1, vcc, %1, %10, vcc\n\t"
       "s_nop 0\n\t"
+#if KHB_RARE
+      // the borrow into limb 2 (probability ~2^-32) is propagated in the rare branch
+      "v_subb_co_u32_e32 %11, vcc, 0, %28, vcc"
+#else
       "v_subbrev_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
       "s_nop 0\n\t"
       "v_subbrev_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
@@ -662,13 +719,26 @@ FM_DEV void fm_sub(Fe& r, const Fe& a, const Fe& b) {
       "s_nop 0\n\t"
       "v_subbrev_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
       "s_nop 0\n\t"
-      "v_subbrev_co_u32_e32 %7, vcc, 0, %7, vcc"
+      "v_subbrev_co_u32_e32 %7, vcc, 0, %7, vcc\n\t"
+      "v_mov_b32 %11, 0"
+#endif
       : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]), "=&v"(d[6]), "=&v"(d[7]),
-        "=&v"(m), "=&v"(k0), "=&v"(k1)
+        "=&v"(m), "=&v"(k0), "=&v"(k1), "=&v"(b2)
       : "v"(a.v[0]), "v"(a.v[1]), "v"(a.v[2]), "v"(a.v[3]), "v"(a.v[4]), "v"(a.v[5]), "v"(a.v[6]), "v"(a.v[7]),
         "v"(b.v[0]), "v"(b.v[1]), "v"(b.v[2]), "v"(b.v[3]), "v"(b.v[4]), "v"(b.v[5]), "v"(b.v[6]), "v"(b.v[7]),
         "v"(0u)
       : "vcc");
+#if KHB_RARE
+  if (fm_any(b2)) {      // b2 = 0xffffffff where the correction borrowed out of limb 1
+    uint32_t bo = b2 & 1u;
+#pragma unroll
+    for (int i = 2; i < 8; ++i) {
+      const uint32_t t = d[i] - bo;
+      bo = (bo && d[i] == 0) ? 1u : 0u;
+      d[i] = t;
+    }
+  }
+#endif
 #pragma unroll
   for (int i = 0; i < 8; ++i) r.v[i] = d[i];
 }
@@ -712,46 +782,47 @@ FM_DEV void fm_canon(Fe& r, const Fe& a) {
 // a + b mod p, lazy: for a < p and b < 2^256 (so a + b < 2^257 - 0x1000003D1) the sum folds its
 // carry back as 2^256 = 0x1000003D1 (mod p) and stays < 2^256.  Feeds a product only.
 FM_DEV void fm_add_lazy(Fe& r, const Fe& a, const Fe& b) {
-  uint32_t s[8], c, k0;
-  asm("v_add_co_u32_e32 %0, vcc, %10, %18\n\t"
+  uint32_t s[8], c;
+  asm("v_add_co_u32_e32 %0, vcc, %9, %17\n\t"
       "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %1, vcc, %11, %19, vcc\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %10, %18, vcc\n\t"
       "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %2, vcc, %12, %20, vcc\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %11, %19, vcc\n\t"
       "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %3, vcc, %13, %21, vcc\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %12, %20, vcc\n\t"
       "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %4, vcc, %14, %22, vcc\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %13, %21, vcc\n\t"
       "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %5, vcc, %15, %23, vcc\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %14, %22, vcc\n\t"
       "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %6, vcc, %16, %24, vcc\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %15, %23, vcc\n\t"
       "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %7, vcc, %17, %25, vcc\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %16, %24, vcc\n\t"
       "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %8, vcc, 0, %26, vcc\n\t"     // c = carry (0/1)
-      "v_mul_u32_u24_e32 %9, 0x3d1, %8\n\t"            // c * 977
-      "v_add_co_u32_e32 %0, vcc, %0, %9\n\t"
-      "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %1, vcc, %1, %8, vcc\n\t"
-      "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
-      "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
-      "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %4, vcc, 0, %4, vcc\n\t"
-      "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %5, vcc, 0, %5, vcc\n\t"
-      "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
-      "s_nop 0\n\t"
-      "v_addc_co_u32_e32 %7, vcc, 0, %7, vcc"
+      "v_addc_co_u32_e32 %8, vcc, 0, %25, vcc"       // c = carry (0/1)
       : "=&v"(s[0]), "=&v"(s[1]), "=&v"(s[2]), "=&v"(s[3]), "=&v"(s[4]), "=&v"(s[5]), "=&v"(s[6]), "=&v"(s[7]),
-        "=&v"(c), "=&v"(k0)
+        "=&v"(c)
       : "v"(a.v[0]), "v"(a.v[1]), "v"(a.v[2]), "v"(a.v[3]), "v"(a.v[4]), "v"(a.v[5]), "v"(a.v[6]), "v"(a.v[7]),
         "v"(b.v[0]), "v"(b.v[1]), "v"(b.v[2]), "v"(b.v[3]), "v"(b.v[4]), "v"(b.v[5]), "v"(b.v[6]), "v"(b.v[7]),
         "v"(0u)
       : "vcc");
+  // fold the carry as 2^256 = 0x1000003D1: limbs 0..1 always; the carry into limb 2 only behind
+  // the rare branch (KHB_RARE)
+  uint32_t c2;
+  asm("v_mul_u32_u24_e32 %2, 0x3d1, %3\n\t"
+      "v_add_co_u32_e32 %0, vcc, %0, %2\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %1, %3, vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e32 %2, vcc, 0, %4, vcc"
+      : "+v"(s[0]), "+v"(s[1]), "=&v"(c2)
+      : "v"(c), "v"(0u)
+      : "vcc");
+#if KHB_RARE
+  if (fm_any(c2)) fm_propagate<2>(s, c2);
+#else
+  fm_propagate<2>(s, c2);
+#endif
 #pragma unroll
   for (int i = 0; i < 8; ++i) r.v[i] = s[i];
 }

@@ -44,7 +44,9 @@ def test_field_ops(eng):
     b = [rand_fe(rng) for _ in range(n)]
     a[0] = 0
     b[1] = 0
-    edges = [0, 1, 2, P - 1, P - 2, P - 977, 2**255, 2**256 - 2**32 - 978, 2**224 - 1, 2**32 - 1, 2**64 - 1]
+    edges = [0, 1, 2, 5, P - 1, P - 2, P - 977, 2**255, 2**256 - 2**32 - 978, 2**224 - 1, 2**32 - 1, 2**64 - 1,
+             2**64, 2**64 + 5, 2**96 - 1, 2**255 + 2**64 - 10]
+    # (5, 2^64): a - b + p borrows out of limb 1 (fm_sub's rare branch, KHB_RARE)
     for k, (x, y) in enumerate((x, y) for x in edges for y in edges):
         a[2 + k], b[2 + k] = x, y
     ab = b"".join(x.to_bytes(32, "big") for x in a)
@@ -63,7 +65,8 @@ def test_fused_field_ops(eng):
     big integers, with operands up to 2^256 - 1 where the contract allows (fe_asm.hpp)."""
     rng = random.Random(5)
     n = 4096
-    lo = [0, 1, P - 1, P - 2, 2**255, 2**32 - 1]                    # < p
+    lo = [0, 1, P - 1, P - 2, 2**255, 2**32 - 1, 2**255 + 2**64 - 10]  # < p
+    # (2^255 + 2^64 - 10) + 2^255: the carry fold carries out of limb 1 (fm_add_lazy's rare branch)
     hi = lo + [P, P + 1, 2**256 - 1, 2**256 - 2, 2**256 - 2**32]     # < 2^256
     a = [rand_fe(rng) for _ in range(n)]
     b = [rng.randrange(2**256) for _ in range(n)]
