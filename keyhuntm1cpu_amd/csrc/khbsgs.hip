@@ -362,9 +362,12 @@ struct GsnTable {
   }
   __device__ __forceinline__ Fe x(uint32_t i) const { return ld(16 * i); }
   __device__ __forceinline__ AffPt pt(uint32_t i) const { return AffPt{ld(16 * i), ld(16 * i + 8)}; }
+  // p - GSn[i].x (0 for x = 0), stored after the 513 points (khb_load_giant_table)
+  __device__ __forceinline__ Fe nx(uint32_t i) const { return ld(16 * KHB_GIANT_TABLE + 8 * i); }
 #else
   __device__ __forceinline__ Fe x(uint32_t i) const { return p[i].x; }
   __device__ __forceinline__ AffPt pt(uint32_t i) const { return p[i]; }
+  __device__ __forceinline__ Fe nx(uint32_t i) const { return reinterpret_cast<const Fe*>(p + KHB_GIANT_TABLE)[i]; }
 #endif
 };
 
@@ -596,12 +599,14 @@ __device__ __forceinline__ void walk_group_g(const ScanArgs& A, ProbeQueue& Q, c
   const size_t S = A.stride;
   const GsnTable gsn{A.gsn};
   const uint32_t base = j * KHB_GROUP;
-  Fe negCx;
+  // the centre enters as p - C.x and p - C.y, so every per-step add/sub is a lazy add
+  Fe negCx, negCy;
   {
     Fe p;
 #pragma unroll
     for (int k = 0; k < 8; ++k) p.v[k] = k == 0 ? KHB_P0 : (k == 1 ? KHB_P1 : 0xFFFFFFFFu);
     fm_sub(negCx, p, C.x);
+    fm_sub(negCy, p, C.y);
   }
   Fe pre = scr_ld(scr + (size_t)(kHalf - 2) * S);
   Fe idx, dx, u, s, x1, x2;
@@ -612,7 +617,7 @@ __device__ __forceinline__ void walk_group_g(const ScanArgs& A, ProbeQueue& Q, c
     fm_add_lazy(dx, gsn.x(kHalf - 1), negCx);
     fm_mul(inv, inv, dx);
     const AffPt g = gsn.pt(kHalf - 1);
-    fm_sub(u, negCx, g.x);
+    fm_add_lazy(u, gsn.nx(kHalf - 1), negCx);
     fm_add_lazy(s, g.y, C.y);
     fm_mul(s, s, idx);
     fm_sqr_add(x1, s, u);
@@ -629,13 +634,13 @@ __device__ __forceinline__ void walk_group_g(const ScanArgs& A, ProbeQueue& Q, c
       idx = inv;
     }
     const AffPt g = gsn.pt(i);
-    fm_sub(u, negCx, g.x);
+    fm_add_lazy(u, gsn.nx(i), negCx);         // nu = -(C.x + GSn.x)
     // C - GSn[i] (pts[511 - i]) and C + GSn[i] (pts[513 + i])
     fm_add_lazy(s, g.y, C.y);
     fm_mul(s, s, idx);
     fm_sqr_add(x1, s, u);
     x_out<kScanG>(A, x1);
-    fm_sub(s, g.y, C.y);
+    fm_add_lazy(s, g.y, negCy);               // GSn.y - C.y
     fm_mul(s, s, idx);
     fm_sqr_add(x2, s, u);
     x_out<kScanG>(A, x2);
@@ -831,15 +836,22 @@ __device__ __forceinline__ void scan_batch(const ScanArgs& A, ProbeQueue& Q, uin
   for (uint32_t g = 0; g < nb; ++g) {
     Fe* const sg = scr + (size_t)g * kHalf * S;
     const Fe cx = sc[2 * g * S];
-    Fe a, dx;
-    fm_sub(a, gsn.x(0), cx);
+    Fe a, dx, negCx;
+    {
+      Fe p;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) p.v[k] = k == 0 ? KHB_P0 : (k == 1 ? KHB_P1 : 0xFFFFFFFFu);
+      fm_sub(negCx, p, cx);
+    }
+    // dx_i = GSn[i].x - C.x as the lazy sum GSn[i].x + (p - C.x) (congruent; feeds products only)
+    fm_add_lazy(a, gsn.x(0), negCx);
     scr_st(sg, a);
     for (uint32_t i = 1; i < kHalf - 1; ++i) {
-      fm_sub(dx, gsn.x(i), cx);
+      fm_add_lazy(dx, gsn.x(i), negCx);
       fm_mul(a, a, dx);
       scr_st(sg + i * S, a);
     }
-    fm_sub(dx, gsn.x(kHalf - 1), cx);
+    fm_add_lazy(dx, gsn.x(kHalf - 1), negCx);
     fm_mul(a, a, dx);
     Fe ac;
     fm_canon(ac, a);
@@ -1260,10 +1272,16 @@ int khb_load_giant_table(khb_ctx* c, const uint8_t* gsn) {
   if (!c || !gsn) return KHB_EINVAL;
   if (c->in_flight) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
-  AffPt h[KHB_GIANT_TABLE];
-  pts_from_be(h, gsn, KHB_GIANT_TABLE);
+  // 513 points, then p - x of each (the walk's negated table, GsnTable::nx)
+  struct {
+    AffPt pt[KHB_GIANT_TABLE];
+    Fe nx[KHB_GIANT_TABLE];
+  } h;
+  pts_from_be(h.pt, gsn, KHB_GIANT_TABLE);
+  const Fe zero{};
+  for (int i = 0; i < KHB_GIANT_TABLE; ++i) fe_sub(h.nx[i], zero, h.pt[i].x);
   if (!c->d_gsn) KHB_TRY(c, hipMalloc(&c->d_gsn, sizeof(h)));
-  KHB_TRY(c, hipMemcpy(c->d_gsn, h, sizeof(h), hipMemcpyHostToDevice));
+  KHB_TRY(c, hipMemcpy(c->d_gsn, &h, sizeof(h), hipMemcpyHostToDevice));
   c->gofs_stale = true;
   return KHB_OK;
 }
