@@ -96,3 +96,6 @@ $(LIBDIR)/variants/libkhbsgs_x%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 $(LIBDIR)/variants/libkhbsgs_xf.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) -DKHB_RARE_FORCE=1 -shared -o $@ $(CSRC)/khbsgs.hip
+$(LIBDIR)/variants/libkhbsgs_nonop.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_NONOP=1 -shared -o $@ $(CSRC)/khbsgs.hip

@@ -30,6 +30,14 @@ namespace khb {
 // (the fold of 2^256 = 0x1000003D1 into a random 256-bit value) runs behind a wave-uniform branch
 // taken only when some lane needs it; the common path stops the chain at the limb that produces
 // the carry.  The branch body is the full propagation, a no-op for lanes whose carry is 0.
+// KHB_NOP: the one wait state between a VCC (carry) write and its VALU reader.  KHB_NONOP=1 drops
+// it: a timing-only build (wrong results) that bounds what the pads cost.
+#if KHB_NONOP
+#define KHB_NOP ""
+#else
+#define KHB_NOP "s_nop 0\n\t"
+#endif
+
 #ifndef KHB_RARE
 #define KHB_RARE 1
 #endif
@@ -55,7 +63,7 @@ FM_DEV uint32_t fm_propagate(uint32_t* r, uint32_t c) {
 // acc += a*b ; c2 += carry-out
 FM_DEV void fm_madc(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
   asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
       : "+v"(acc), "+v"(c2)
       : "v"(a), "v"(b)
@@ -95,7 +103,7 @@ FM_DEV void fm_mul512(uint32_t t[16], const uint32_t* a, const uint32_t* b) {
 // acc += a*b; cw = carry-out (first carry of a column: no zero-initialisation needed)
 FM_DEV void fm_madc_first(uint64_t& acc, uint32_t& cw, uint32_t a, uint32_t b) {
   asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, 0, %4, vcc"
       : "+v"(acc), "=v"(cw)
       : "v"(a), "v"(b), "v"(0u)
@@ -120,33 +128,33 @@ FM_DEV void fm_fold_cols(uint32_t t[16], const uint64_t A[15], uint32_t cw13) {
 #define FM_HI(k) "v"((uint32_t)(A[k] >> 32))
   t[0] = (uint32_t)A[0];
   asm("v_add_co_u32_e32 %0, vcc, %15, %16\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, %17, %18, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %2, vcc, %19, %20, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %3, vcc, %21, %22, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %4, vcc, %23, %24, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %5, vcc, %25, %26, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %6, vcc, %27, %28, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %7, vcc, %29, %30, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %8, vcc, %31, %32, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %9, vcc, %33, %34, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %10, vcc, %35, %36, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %11, vcc, %37, %38, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %12, vcc, %39, %40, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %13, vcc, %41, %42, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %14, vcc, %43, %44, vcc"
       : "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7]),
         "=&v"(t[8]), "=&v"(t[9]), "=&v"(t[10]), "=&v"(t[11]), "=&v"(t[12]), "=&v"(t[13]), "=&v"(t[14]),
@@ -183,7 +191,7 @@ FM_DEV void fm_mul512x(uint32_t t[16], const uint32_t* a, const uint32_t* b) {
 // column k+1, which has the same weight.  seed <= 8, so seeding never overflows a column.
 FM_DEV void fm_fold_step(uint32_t& t, uint32_t& seed, uint64_t cur, uint64_t prev, uint32_t cw) {
   asm("v_add_co_u32_e32 %0, vcc, %2, %3\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, 0, %4, vcc"
       : "=&v"(t), "=v"(seed)
       : "v"((uint32_t)cur), "v"((uint32_t)(prev >> 32)), "v"(cw)
@@ -212,7 +220,7 @@ FM_DEV void fm_mul512p(uint32_t t[16], const uint32_t* a, const uint32_t* b) {
   cur = (uint64_t)seed;
   cur += (uint64_t)a[7] * b[7];
   asm("v_add_co_u32_e32 %0, vcc, %2, %3\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, %4, %5, vcc"
       : "=&v"(t[14]), "=v"(t[15])
       : "v"((uint32_t)cur), "v"((uint32_t)(prev >> 32)), "v"(cw[13]), "v"((uint32_t)(cur >> 32))
@@ -243,9 +251,9 @@ FM_DEV void fm_sq_word_first(uint32_t& t, uint64_t& sU, uint64_t& sT, uint32_t d
 }
 FM_DEV void fm_sq_word(uint32_t& t, uint64_t& sU, uint64_t& sT, uint32_t d, uint32_t c) {
   uint32_t u;
-  asm("s_nop 0\n\t"
+  asm(KHB_NOP
       "v_addc_co_u32_e64 %0, %2, %4, %5, %2\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e64 %1, %3, %0, %5, %3"
       : "=&v"(u), "=v"(t), "+s"(sU), "+s"(sT)
       : "v"(d), "v"(c));
@@ -340,35 +348,35 @@ FM_DEV void fm_sqr512x(uint32_t t[16], const uint32_t* a) {
   // t = D + c + c
   uint32_t u[16];
   asm("v_add_co_u32_e32 %0, vcc, %16, %32\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, %17, %33, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %2, vcc, %18, %34, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %3, vcc, %19, %35, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %4, vcc, %20, %36, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %5, vcc, %21, %37, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %6, vcc, %22, %38, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %7, vcc, %23, %39, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %8, vcc, %24, %40, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %9, vcc, %25, %41, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %10, vcc, %26, %42, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %11, vcc, %27, %43, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %12, vcc, %28, %44, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %13, vcc, %29, %45, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %14, vcc, %30, %46, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %15, vcc, %31, %47, vcc"
       : "=&v"(u[0]), "=&v"(u[1]), "=&v"(u[2]), "=&v"(u[3]), "=&v"(u[4]), "=&v"(u[5]), "=&v"(u[6]), "=&v"(u[7]),
         "=&v"(u[8]), "=&v"(u[9]), "=&v"(u[10]), "=&v"(u[11]), "=&v"(u[12]), "=&v"(u[13]), "=&v"(u[14]),
@@ -381,35 +389,35 @@ FM_DEV void fm_sqr512x(uint32_t t[16], const uint32_t* a) {
         "v"(c[10]), "v"(c[11]), "v"(c[12]), "v"(c[13]), "v"(c[14]), "v"(c[15])
       : "vcc");
   asm("v_add_co_u32_e32 %0, vcc, %0, %16\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, %1, %17, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %2, vcc, %2, %18, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %3, vcc, %3, %19, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %4, vcc, %4, %20, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %5, vcc, %5, %21, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %6, vcc, %6, %22, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %7, vcc, %7, %23, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %8, vcc, %8, %24, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %9, vcc, %9, %25, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %10, vcc, %10, %26, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %11, vcc, %11, %27, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %12, vcc, %12, %28, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %13, vcc, %13, %29, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %14, vcc, %14, %30, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %15, vcc, %15, %31, vcc"
       : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]),
         "+v"(u[8]), "+v"(u[9]), "+v"(u[10]), "+v"(u[11]), "+v"(u[12]), "+v"(u[13]), "+v"(u[14]), "+v"(u[15])
@@ -432,21 +440,21 @@ FM_DEV void fm_reduce(Fe& r, const uint32_t t[16]) {
   uint32_t T[10];
   asm("v_mov_b32 %0, %10\n\t"
       "v_add_co_u32_e32 %1, vcc, %11, %18\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %2, vcc, %12, %19, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %3, vcc, %13, %20, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %4, vcc, %14, %21, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %5, vcc, %15, %22, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %6, vcc, %16, %23, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %7, vcc, %17, %24, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %8, vcc, 0, %25, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %9, vcc, 0, %26, vcc"
       : "=&v"(T[0]), "=&v"(T[1]), "=&v"(T[2]), "=&v"(T[3]), "=&v"(T[4]), "=&v"(T[5]), "=&v"(T[6]), "=&v"(T[7]),
         "=&v"(T[8]), "=&v"(T[9])
@@ -465,21 +473,21 @@ FM_DEV void fm_reduce_add(Fe& r, const uint32_t t[16], const Fe& w) {
   const uint32_t* H = t + 8;
   uint32_t U[9], T[10];
   asm("v_add_co_u32_e32 %0, vcc, %9, %17\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, %10, %18, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %2, vcc, %11, %19, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %3, vcc, %12, %20, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %4, vcc, %13, %21, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %5, vcc, %14, %22, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %6, vcc, %15, %23, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %7, vcc, %16, %24, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %8, vcc, 0, %25, vcc"
       : "=&v"(U[0]), "=&v"(U[1]), "=&v"(U[2]), "=&v"(U[3]), "=&v"(U[4]), "=&v"(U[5]), "=&v"(U[6]), "=&v"(U[7]),
         "=&v"(U[8])
@@ -489,21 +497,21 @@ FM_DEV void fm_reduce_add(Fe& r, const uint32_t t[16], const Fe& w) {
       : "vcc");
   T[0] = U[0];
   asm("v_add_co_u32_e32 %0, vcc, %9, %17\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, %10, %18, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %2, vcc, %11, %19, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %3, vcc, %12, %20, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %4, vcc, %13, %21, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %5, vcc, %14, %22, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %6, vcc, %15, %23, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %7, vcc, %16, %24, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %8, vcc, 0, %25, vcc"
       : "=&v"(T[1]), "=&v"(T[2]), "=&v"(T[3]), "=&v"(T[4]), "=&v"(T[5]), "=&v"(T[6]), "=&v"(T[7]), "=&v"(T[8]),
         "=&v"(T[9])
@@ -522,21 +530,21 @@ FM_DEV void fm_reduce_T(Fe& r, const uint32_t T[10], const uint32_t* H) {
   uint32_t R[8], R8, R9;
   asm("v_mov_b32 %0, %10\n\t"
       "v_add_co_u32_e32 %1, vcc, %11, %12\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %2, vcc, %13, %14, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %3, vcc, %15, %16, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %4, vcc, %17, %18, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %5, vcc, %19, %20, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %6, vcc, %21, %22, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %7, vcc, %23, %24, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %8, vcc, %25, %26, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %9, vcc, 0, %27, vcc"
       : "=&v"(R[0]), "=&v"(R[1]), "=&v"(R[2]), "=&v"(R[3]), "=&v"(R[4]), "=&v"(R[5]), "=&v"(R[6]), "=&v"(R[7]),
         "=&v"(R8), "=&v"(R9)
@@ -560,11 +568,11 @@ FM_DEV void fm_reduce_T(Fe& r, const uint32_t T[10], const uint32_t* H) {
   // a wrap past 2^256 (~2^-212) folded, only in the rare branch.
   uint32_t c3;
   asm("v_add_co_u32_e32 %0, vcc, %0, %4\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, %1, %5, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %2, vcc, %2, %6, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %3, vcc, 0, %7, vcc"
       : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "=&v"(c3)
       : "v"((uint32_t)u), "v"((uint32_t)w), "v"(w2), "v"(0u)
@@ -583,21 +591,21 @@ FM_DEV void fm_reduce_T(Fe& r, const uint32_t T[10], const uint32_t* H) {
   return;
 #endif
   asm("v_add_co_u32_e32 %0, vcc, %0, %9\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, %1, %10, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %2, vcc, %2, %11, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %4, vcc, 0, %4, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %5, vcc, 0, %5, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %7, vcc, 0, %7, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %8, vcc, 0, %12, vcc"
       : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]), "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]), "=&v"(c)
       : "v"((uint32_t)u), "v"((uint32_t)w), "v"(w2), "v"(0u)
@@ -606,11 +614,11 @@ FM_DEV void fm_reduce_T(Fe& r, const uint32_t T[10], const uint32_t* H) {
   // more (limbs 0..3 suffice: the sum stays < 2^68).
   const uint32_t k0 = c * 977u;
   asm("v_add_co_u32_e32 %0, vcc, %0, %4\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, %1, %5, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %3, vcc, 0, %3, vcc"
       : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3])
       : "v"(k0), "v"(c)
@@ -682,43 +690,43 @@ FM_DEV void fm_sqr_generic(Fe& r, const Fe& a) {
 FM_DEV void fm_sub(Fe& r, const Fe& a, const Fe& b) {
   uint32_t d[8], m, k0, k1, b2;
   asm("v_sub_co_u32_e32 %0, vcc, %12, %20\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_subb_co_u32_e32 %1, vcc, %13, %21, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_subb_co_u32_e32 %2, vcc, %14, %22, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_subb_co_u32_e32 %3, vcc, %15, %23, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_subb_co_u32_e32 %4, vcc, %16, %24, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_subb_co_u32_e32 %5, vcc, %17, %25, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_subb_co_u32_e32 %6, vcc, %18, %26, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_subb_co_u32_e32 %7, vcc, %19, %27, vcc\n\t"
       // m = borrow ? 0xffffffff : 0 ; subtract (0x1000003D1 & m), i.e. add p on borrow
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_subb_co_u32_e32 %8, vcc, 0, %28, vcc\n\t"
       "v_and_b32_e32 %9, 0x3d1, %8\n\t"
       "v_and_b32_e32 %10, 1, %8\n\t"
       "v_sub_co_u32_e32 %0, vcc, %0, %9\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_subb_co_u32_e32 %1, vcc, %1, %10, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
 #if KHB_RARE
       // the borrow into limb 2 (probability ~2^-32) is propagated in the rare branch
       "v_subb_co_u32_e32 %11, vcc, 0, %28, vcc"
 #else
       "v_subbrev_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_subbrev_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_subbrev_co_u32_e32 %4, vcc, 0, %4, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_subbrev_co_u32_e32 %5, vcc, 0, %5, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_subbrev_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_subbrev_co_u32_e32 %7, vcc, 0, %7, vcc\n\t"
       "v_mov_b32 %11, 0"
 #endif
@@ -747,21 +755,21 @@ FM_DEV void fm_sub(Fe& r, const Fe& a, const Fe& b) {
 FM_DEV uint32_t fm_add_k(uint32_t t[8], const uint32_t s[8]) {
   uint32_t c;
   asm("v_add_co_u32_e32 %0, vcc, 0x3d1, %9\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, 1, %10, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %2, vcc, 0, %11, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %3, vcc, 0, %12, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %4, vcc, 0, %13, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %5, vcc, 0, %14, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %6, vcc, 0, %15, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %7, vcc, 0, %16, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %8, vcc, 0, %17, vcc"
       : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7]),
         "=&v"(c)
@@ -784,21 +792,21 @@ FM_DEV void fm_canon(Fe& r, const Fe& a) {
 FM_DEV void fm_add_lazy(Fe& r, const Fe& a, const Fe& b) {
   uint32_t s[8], c;
   asm("v_add_co_u32_e32 %0, vcc, %9, %17\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, %10, %18, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %2, vcc, %11, %19, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %3, vcc, %12, %20, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %4, vcc, %13, %21, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %5, vcc, %14, %22, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %6, vcc, %15, %23, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %7, vcc, %16, %24, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %8, vcc, 0, %25, vcc"       // c = carry (0/1)
       : "=&v"(s[0]), "=&v"(s[1]), "=&v"(s[2]), "=&v"(s[3]), "=&v"(s[4]), "=&v"(s[5]), "=&v"(s[6]), "=&v"(s[7]),
         "=&v"(c)
@@ -811,9 +819,9 @@ FM_DEV void fm_add_lazy(Fe& r, const Fe& a, const Fe& b) {
   uint32_t c2;
   asm("v_mul_u32_u24_e32 %2, 0x3d1, %3\n\t"
       "v_add_co_u32_e32 %0, vcc, %0, %2\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, %1, %3, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %2, vcc, 0, %4, vcc"
       : "+v"(s[0]), "+v"(s[1]), "=&v"(c2)
       : "v"(c), "v"(0u)
@@ -831,21 +839,21 @@ FM_DEV void fm_add_lazy(Fe& r, const Fe& a, const Fe& b) {
 FM_DEV void fm_add(Fe& r, const Fe& a, const Fe& b) {
   uint32_t s[8], c;
   asm("v_add_co_u32_e32 %0, vcc, %9, %17\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %1, vcc, %10, %18, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %2, vcc, %11, %19, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %3, vcc, %12, %20, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %4, vcc, %13, %21, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %5, vcc, %14, %22, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %6, vcc, %15, %23, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %7, vcc, %16, %24, vcc\n\t"
-      "s_nop 0\n\t"
+      KHB_NOP
       "v_addc_co_u32_e32 %8, vcc, 0, %25, vcc"
       : "=&v"(s[0]), "=&v"(s[1]), "=&v"(s[2]), "=&v"(s[3]), "=&v"(s[4]), "=&v"(s[5]), "=&v"(s[6]), "=&v"(s[7]),
         "=&v"(c)

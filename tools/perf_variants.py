@@ -56,7 +56,7 @@ for rnd in range(int(os.environ.get("ROUNDS", "3"))):
         c, d, st = e.scan(centres, 0, t.cycles)
         times[n].append(st.kernel_ms)
         ncand[n] = len(c)
-        if "_p" in n.split()[0]:      # probe experiments: candidates not comparable
+        if "_p" in n.split()[0] or "nonop" in n:   # probe / timing-only experiments: not comparable
             continue
         s = sorted(c)
         ref.setdefault(g, s)
