@@ -17,6 +17,7 @@
 #include <string.h>
 #include <stdlib.h>
 #include <new>
+#include <vector>
 #include "../../include/khbsgs.h"
 #include "device/fe.hpp"
 #include "device/fe_asm.hpp"
@@ -51,6 +52,9 @@ struct AffPt {
 #endif
 #ifndef KHB_FUSE
 #define KHB_FUSE 1                // -m bsgs walk: x = s^2 + nu fused into the squaring's reduction
+#endif
+#ifndef KHB_GATE1
+#define KHB_GATE1 0               // log2 bytes of an L2-sized stage-1 fold of the level-0 gate (0 = none)
 #endif
 #ifndef KHB_WAVES_PER_SIMD
 #define KHB_WAVES_PER_SIMD 4      // occupancy target of k_giant_scan (launch bounds); w4 measured best
@@ -132,6 +136,10 @@ struct ScanArgs {
   uint32_t gate_probes;
   uint64_t glimit;
   uint32_t gate_mask;                  // blocks - 1
+  // stage-1 gate (KHB_GATE1): the level-0 gate OR-folded to (gate1_mask + 1) blocks, block i of
+  // the fold = OR of blocks j of the gate with j & gate1_mask == i; null = no stage 1
+  const uint8_t* __restrict__ gate1;
+  uint32_t gate1_mask;
   uint64_t job_keys;                   // baby steps per job
   uint64_t n_items;
   uint32_t n_jobs, group_begin, group_end, gpl, lanes_per_job, stride, cand_cap, degen_cap;
@@ -262,8 +270,29 @@ __device__ __forceinline__ GatePend gate_issue(const ScanArgs& A, const Fe& x) {
 // blocks are loaded before either is waited for; survivors (~0.04 % of x) go to the queue.
 __device__ __forceinline__ void gate_pair(const ScanArgs& A, ProbeQueue& Q, const Fe& x1, uint32_t step1, bool has2,
                                           const Fe& x2, uint32_t step2, uint32_t job) {
+#if KHB_GATE1
+  bool h1, h2;
+  if (A.gate1) {
+    // stage 1 (L2-resident fold); the full gate's line is fetched only for its survivors
+    const uint32_t b1 = gate_bits(A, x1), b2 = gate_bits(A, x2);
+    const uint2 f1 = reinterpret_cast<const uint2*>(A.gate1)[x1.v[0] & A.gate1_mask];
+    const uint2 f2 = reinterpret_cast<const uint2*>(A.gate1)[x2.v[0] & A.gate1_mask];
+    const bool s1 = gate_block_pass(f1.x, f1.y, b1), s2 = has2 && gate_block_pass(f2.x, f2.y, b2);
+    if (__ballot(s1 || s2) == 0) return;
+    uint2 w1 = make_uint2(0u, 0u), w2 = make_uint2(0u, 0u);
+    if (s1) w1 = reinterpret_cast<const uint2*>(A.gate)[x1.v[0] & A.gate_mask];
+    if (s2) w2 = reinterpret_cast<const uint2*>(A.gate)[x2.v[0] & A.gate_mask];
+    h1 = s1 && gate_block_pass(w1.x, w1.y, b1);
+    h2 = s2 && gate_block_pass(w2.x, w2.y, b2);
+  } else {
+    const GatePend q1 = gate_issue(A, x1), q2 = gate_issue(A, x2);
+    h1 = q1.pass();
+    h2 = has2 && q2.pass();
+  }
+#else
   const GatePend q1 = gate_issue(A, x1), q2 = gate_issue(A, x2);
   const bool h1 = q1.pass(), h2 = has2 && q2.pass();
+#endif
   if (__ballot(h1 || h2) == 0) return;
   q_push(Q, h1, x1, job, step1);
   q_drain(A, Q, kDrainAt);
@@ -1029,6 +1058,8 @@ struct khb_ctx {
   uint8_t* d_bloom = nullptr;
   BloomGeom geom{};
   uint8_t* d_gate = nullptr;           // level-0 gate (khb_load_gate), null = none
+  uint8_t* d_gate1 = nullptr;          // its stage-1 fold (KHB_GATE1), null = none
+  uint32_t gate1_mask = 0;
   uint32_t gate_mask = 0, gate_probes = 0;
   AffPt* d_gsn = nullptr;
   AffPt* d_offs = nullptr;
@@ -1094,6 +1125,8 @@ ScanArgs make_args(khb_ctx* c, uint32_t n_jobs, uint32_t group_begin, uint32_t g
   A.gate = c->d_gate;
   A.gate_mask = c->gate_mask;
   A.gate_probes = c->gate_probes;
+  A.gate1 = c->d_gate1;
+  A.gate1_mask = c->gate1_mask;
   A.gsn = c->d_gsn;
   A.offs = c->d_offs;
   A.gofs = c->gpl == 1 ? c->d_offs : c->d_gofs;
@@ -1216,6 +1249,7 @@ int khb_close(khb_ctx* c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   hipFree(c->d_bloom);
   hipFree(c->d_gate);
+  hipFree(c->d_gate1);
   hipFree(c->d_gsn);
   hipFree(c->d_offs);
   hipFree(c->d_gofs);
@@ -1241,13 +1275,24 @@ int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t 
   if (c->in_flight) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
   if (c->d_gate) { hipFree(c->d_gate); c->d_gate = nullptr; }
-  c->gate_mask = 0;
+  if (c->d_gate1) { hipFree(c->d_gate1); c->d_gate1 = nullptr; }
+  c->gate_mask = c->gate1_mask = 0;
   if (!gate) return KHB_OK;
   const size_t bytes = (size_t)1 << (log2_bits - 3);
   KHB_TRY(c, hipMalloc(&c->d_gate, bytes));
   KHB_TRY(c, hipMemcpy(c->d_gate, gate, bytes, hipMemcpyHostToDevice));
   c->gate_mask = (uint32_t)((1ull << (log2_bits - 6)) - 1);
   c->gate_probes = probes;
+  if (KHB_GATE1 && (size_t)1 << KHB_GATE1 < bytes) {
+    // stage 1: the gate OR-folded to 2^KHB_GATE1 bytes (a superset: no member is ever dropped)
+    const size_t nb1 = ((size_t)1 << KHB_GATE1) / 8, nb = bytes / 8;
+    std::vector<uint64_t> f(nb1, 0);
+    const uint64_t* g = reinterpret_cast<const uint64_t*>(gate);
+    for (size_t j = 0; j < nb; ++j) f[j & (nb1 - 1)] |= g[j];
+    KHB_TRY(c, hipMalloc(&c->d_gate1, nb1 * 8));
+    KHB_TRY(c, hipMemcpy(c->d_gate1, f.data(), nb1 * 8, hipMemcpyHostToDevice));
+    c->gate1_mask = (uint32_t)(nb1 - 1);
+  }
   return KHB_OK;
 }
 
