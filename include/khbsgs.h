@@ -96,6 +96,13 @@ int khb_load_bloom(khb_ctx* ctx, const uint8_t* bf_concat, uint64_t bytes_per_su
  * gate NULL removes it; log2_bits in [13, 32]; probes in [1, KHB_GATE_MAX_PROBES]. */
 #define KHB_GATE_MAX_PROBES 3
 int khb_load_gate(khb_ctx* ctx, const uint8_t* gate, uint32_t log2_bits, uint32_t probes);
+/* Stage-1 fold for gates loaded after this call: a gate larger than 2^log2_bytes bytes is also kept
+ * OR-folded to 2^log2_bytes bytes (block i of the fold = OR of the gate's blocks j with
+ * j mod (2^log2_bytes / 8) == i).  x tests its block of the fold first and reads its block of the
+ * full gate only when those bits are all set: the same candidates, fewer random reads of a gate
+ * that does not fit the Infinity Cache beside the level-1 bloom (k >= 4).  0 = no stage 1;
+ * otherwise log2_bytes in [10, 31].  Default 25 (32 MiB: no fold at k = 1, a 4x fold at k = 4). */
+int khb_set_gate_stage1(khb_ctx* ctx, uint32_t log2_bytes);
 /* GSn[0..511] and _2GSn (keyhunt.cpp:1325-1338), 513 affine points x||y BE. */
 int khb_load_giant_table(khb_ctx* ctx, const uint8_t* gsn_xy_be);
 /* Lane start offsets: offs[m] = (m*groups_per_lane) * _2GSn, m in [0, n) (offs[0] unused: the

@@ -54,7 +54,7 @@ struct AffPt {
 #define KHB_FUSE 1                // -m bsgs walk: x = s^2 + nu fused into the squaring's reduction
 #endif
 #ifndef KHB_GATE1
-#define KHB_GATE1 0               // log2 bytes of an L2-sized stage-1 fold of the level-0 gate (0 = none)
+#define KHB_GATE1 25              // default log2 bytes of the stage-1 fold of a larger level-0 gate (0 = none)
 #endif
 #ifndef KHB_WAVES_PER_SIMD
 #define KHB_WAVES_PER_SIMD 4      // occupancy target of k_giant_scan (launch bounds); w4 measured best
@@ -75,8 +75,10 @@ enum : int {
   kAddrDump = 5,   // -m address parity: write every x||y
   kBaby = 6,       // baby-step table build: bloom_add of every x into L1/L2/L3 + bPtable records
   kScanG = 7,      // -m bsgs with a level-0 gate (the product path: walk_group_g)
+  kScanG1 = 8,     // kScanG with the gate's stage-1 fold in front (khb_set_gate_stage1; k >= 4)
 };
-constexpr bool is_scan(int m) { return m == kScan || m == kScanG; }
+constexpr bool is_gated(int m) { return m == kScanG || m == kScanG1; }
+constexpr bool is_scan(int m) { return m == kScan || is_gated(m); }
 constexpr bool is_addr(int m) { return m >= kAddrU && m <= kAddrDump; }
 constexpr bool needs_y(int m) { return m == kAddrU || m == kAddrB || m == kAddrDump; }
 constexpr bool is_dump(int m) { return m == kDump || m == kAddrDump || m == kBaby; }
@@ -136,7 +138,7 @@ struct ScanArgs {
   uint32_t gate_probes;
   uint64_t glimit;
   uint32_t gate_mask;                  // blocks - 1
-  // stage-1 gate (KHB_GATE1): the level-0 gate OR-folded to (gate1_mask + 1) blocks, block i of
+  // stage-1 gate (khb_set_gate_stage1): the level-0 gate OR-folded to (gate1_mask + 1) blocks, block i of
   // the fold = OR of blocks j of the gate with j & gate1_mask == i; null = no stage 1
   const uint8_t* __restrict__ gate1;
   uint32_t gate1_mask;
@@ -268,11 +270,11 @@ __device__ __forceinline__ GatePend gate_issue(const ScanArgs& A, const Fe& x) {
 
 // kScanG: gate test of one walk step's two x (x2 absent at step 511: has2 = false, uniform).  Both
 // blocks are loaded before either is waited for; survivors (~0.04 % of x) go to the queue.
+template <bool STAGE1>
 __device__ __forceinline__ void gate_pair(const ScanArgs& A, ProbeQueue& Q, const Fe& x1, uint32_t step1, bool has2,
                                           const Fe& x2, uint32_t step2, uint32_t job) {
-#if KHB_GATE1
   bool h1, h2;
-  if (A.gate1) {
+  if constexpr (STAGE1) {
     // stage 1 (L2-resident fold); the full gate's line is fetched only for its survivors
     const uint32_t b1 = gate_bits(A, x1), b2 = gate_bits(A, x2);
     const uint2 f1 = reinterpret_cast<const uint2*>(A.gate1)[x1.v[0] & A.gate1_mask];
@@ -289,10 +291,6 @@ __device__ __forceinline__ void gate_pair(const ScanArgs& A, ProbeQueue& Q, cons
     h1 = q1.pass();
     h2 = has2 && q2.pass();
   }
-#else
-  const GatePend q1 = gate_issue(A, x1), q2 = gate_issue(A, x2);
-  const bool h1 = q1.pass(), h2 = has2 && q2.pass();
-#endif
   if (__ballot(h1 || h2) == 0) return;
   q_push(Q, h1, x1, job, step1);
   q_drain(A, Q, kDrainAt);
@@ -489,7 +487,7 @@ __device__ __forceinline__ void baby_point(const ScanArgs& A, const Fe& x, uint3
 // per wave), and the drain canonicalises its survivors before hashing.
 template <int MODE>
 __device__ __forceinline__ void x_out(const ScanArgs& A, Fe& x) {
-  if ((MODE == kScan && A.gate) || MODE == kScanG) {
+  if ((MODE == kScan && A.gate) || is_gated(MODE)) {
     if (x.v[7] == 0xffffffffu) fm_canon(x, x);
   } else {
     fm_canon(x, x);
@@ -623,6 +621,7 @@ __device__ __forceinline__ void walk_group(const ScanArgs& A, ProbeQueue& Q, con
 // each step's two x gate-tested together (gate_pair).  The first step is peeled and the prefix
 // load is unconditional, so the loop body issues the same vector-memory sequence every time and
 // the waitcnt pass waits for exactly the operand it needs.
+template <bool STAGE1>
 __device__ __forceinline__ void walk_group_g(const ScanArgs& A, ProbeQueue& Q, const AffPt& C, Fe inv,
                                              uint32_t job, uint32_t j, const Fe* scr) {
   const size_t S = A.stride;
@@ -651,7 +650,7 @@ __device__ __forceinline__ void walk_group_g(const ScanArgs& A, ProbeQueue& Q, c
     fm_mul(s, s, idx);
     fm_sqr_add(x1, s, u);
     x_out<kScanG>(A, x1);
-    gate_pair(A, Q, x1, base, false, x1, 0, job);
+    gate_pair<STAGE1>(A, Q, x1, base, false, x1, 0, job);
   }
   for (int i = (int)kHalf - 2; i >= 0; --i) {
     if (i > 0) {
@@ -673,7 +672,7 @@ __device__ __forceinline__ void walk_group_g(const ScanArgs& A, ProbeQueue& Q, c
     fm_mul(s, s, idx);
     fm_sqr_add(x2, s, u);
     x_out<kScanG>(A, x2);
-    gate_pair(A, Q, x1, base + kHalf - 1 - (uint32_t)i, true, x2, base + kHalf + 1 + (uint32_t)i, job);
+    gate_pair<STAGE1>(A, Q, x1, base + kHalf - 1 - (uint32_t)i, true, x2, base + kHalf + 1 + (uint32_t)i, job);
   }
   probe<false>(A, Q, C.x, job, j, kHalf);        // the centre, pts[512]
 }
@@ -911,8 +910,8 @@ __device__ __forceinline__ void scan_batch(const ScanArgs& A, ProbeQueue& Q, uin
     Fe* const sg = scr + (size_t)g * kHalf * S;
     asm volatile("" ::: "memory");
     const AffPt C{sc[2 * g * S], sc[(2 * g + 1) * S]};
-    if constexpr (MODE == kScanG)
-      walk_group_g(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
+    if constexpr (is_gated(MODE))
+      walk_group_g<MODE == kScanG1>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
     else
       walk_group<MODE>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
     if (MODE != kDump && ((degen >> g) & 1u)) {
@@ -1058,8 +1057,9 @@ struct khb_ctx {
   uint8_t* d_bloom = nullptr;
   BloomGeom geom{};
   uint8_t* d_gate = nullptr;           // level-0 gate (khb_load_gate), null = none
-  uint8_t* d_gate1 = nullptr;          // its stage-1 fold (KHB_GATE1), null = none
+  uint8_t* d_gate1 = nullptr;          // its stage-1 fold, null = none
   uint32_t gate1_mask = 0;
+  uint32_t gate1_log2 = KHB_GATE1;     // khb_set_gate_stage1: fold size for gates loaded later
   uint32_t gate_mask = 0, gate_probes = 0;
   AffPt* d_gsn = nullptr;
   AffPt* d_offs = nullptr;
@@ -1283,9 +1283,9 @@ int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t 
   KHB_TRY(c, hipMemcpy(c->d_gate, gate, bytes, hipMemcpyHostToDevice));
   c->gate_mask = (uint32_t)((1ull << (log2_bits - 6)) - 1);
   c->gate_probes = probes;
-  if (KHB_GATE1 && (size_t)1 << KHB_GATE1 < bytes) {
-    // stage 1: the gate OR-folded to 2^KHB_GATE1 bytes (a superset: no member is ever dropped)
-    const size_t nb1 = ((size_t)1 << KHB_GATE1) / 8, nb = bytes / 8;
+  if (c->gate1_log2 && (size_t)1 << c->gate1_log2 < bytes) {
+    // stage 1: the gate OR-folded to 2^gate1_log2 bytes (a superset: no member is ever dropped)
+    const size_t nb1 = ((size_t)1 << c->gate1_log2) / 8, nb = bytes / 8;
     std::vector<uint64_t> f(nb1, 0);
     const uint64_t* g = reinterpret_cast<const uint64_t*>(gate);
     for (size_t j = 0; j < nb; ++j) f[j & (nb1 - 1)] |= g[j];
@@ -1293,6 +1293,13 @@ int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t 
     KHB_TRY(c, hipMemcpy(c->d_gate1, f.data(), nb1 * 8, hipMemcpyHostToDevice));
     c->gate1_mask = (uint32_t)(nb1 - 1);
   }
+  return KHB_OK;
+}
+
+int khb_set_gate_stage1(khb_ctx* c, uint32_t log2_bytes) {
+  if (!c || (log2_bytes && (log2_bytes < 10 || log2_bytes > 31))) return KHB_EINVAL;
+  if (c->in_flight) return KHB_EBUSY;
+  c->gate1_log2 = log2_bytes;
   return KHB_OK;
 }
 
@@ -1362,7 +1369,9 @@ int khb_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t gro
   ScanArgs A = make_args(c, n_jobs, group_begin, group_count, kBatch);
   const uint32_t blocks = c->lanes / kBlock;
   KHB_TRY(c, hipEventRecord(c->ev0, c->stream));
-  if (c->d_gate)
+  if (c->d_gate1)
+    hipLaunchKernelGGL(k_giant_scan<kScanG1>, dim3(blocks), dim3(kBlock), 0, c->stream, A);
+  else if (c->d_gate)
     hipLaunchKernelGGL(k_giant_scan<kScanG>, dim3(blocks), dim3(kBlock), 0, c->stream, A);
   else
     hipLaunchKernelGGL(k_giant_scan<kScan>, dim3(blocks), dim3(kBlock), 0, c->stream, A);

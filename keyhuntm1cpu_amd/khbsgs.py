@@ -64,6 +64,8 @@ def lib(path: str | None = None) -> C.CDLL:
         L.khb_load_bloom.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, C.c_uint64, C.c_uint32]
         L.khb_load_giant_table.argtypes = [C.c_void_p, C.c_char_p]
         L.khb_load_gate.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32]
+        if hasattr(L, "khb_set_gate_stage1"):    # absent only in older timing builds (tools/perf_variants.py)
+            L.khb_set_gate_stage1.argtypes = [C.c_void_p, C.c_uint32]
         L.khb_load_lane_offsets.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32]
         L.khb_submit.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]
         L.khb_collect.argtypes = [C.c_void_p, P(Cand), C.c_uint32, P(Degenerate), C.c_uint32, P(Stats)]
@@ -143,6 +145,10 @@ class Engine:
         if gate is not None:
             assert len(gate) == (1 << log2_bits) // 8
         _check(self.L.khb_load_gate(self.h, gate, log2_bits if gate is not None else 0, probes), self.h, self.L)
+
+    def set_gate_stage1(self, log2_bytes: int) -> None:
+        """Stage-1 fold size (2^log2_bytes bytes) for gates loaded afterwards; 0 = none."""
+        _check(self.L.khb_set_gate_stage1(self.h, log2_bytes), self.h, self.L)
 
     def load_giant_table(self, gsn: bytes) -> None:
         assert len(gsn) == 513 * 64

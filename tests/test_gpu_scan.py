@@ -206,7 +206,7 @@ def test_gate_candidates_exact(eng, bs32, ora, probes):
     are all set.  A dense synthetic L1 (each bit set with p = 0.97, so ~54 % of all x pass) and a
     random gate (each bit set with p = 0.5^(1/probes), so about half of all x pass it) exercise
     both paths on every x of four chunks; without the gate the same scan returns the plain L1
-    candidates."""
+    candidates, and with a stage-1 fold of the gate in front (khb_set_gate_stage1) the gated ones."""
     gpl = 4
     load_tables(eng, bs32, gpl)
     _, nb, bits, hashes = bs32.bloom_concat(1)
@@ -231,15 +231,19 @@ def test_gate_candidates_exact(eng, bs32, ora, probes):
         l1_ref.append(l1)
         gate_ref.append(gt)
     try:
-        for use_gate, ref in ((False, l1_ref), (True, gate_ref)):
+        # stage 1 = 12: the 8 KiB gate is also kept folded to 4 KiB and tested there first
+        # (khb_set_gate_stage1); the candidates must not change
+        for use_gate, stage1, ref in ((False, 0, l1_ref), (True, 0, gate_ref), (True, 12, gate_ref)):
+            eng.set_gate_stage1(stage1)
             eng.load_gate(gate if use_gate else None, lg, probes)
             got, degen, _ = eng.scan(b"".join(centres), 0, bs32.cycles)
             per_job = [[] for _ in centres]
             for job, a in got:
                 per_job[job].append(a)
-            assert [sorted(x) for x in per_job] == ref, use_gate
+            assert [sorted(x) for x in per_job] == ref, (use_gate, stage1)
         assert 0.4 < sum(map(len, gate_ref)) / sum(map(len, l1_ref)) < 0.6
         assert sum(map(len, l1_ref)) > 100000
     finally:
+        eng.set_gate_stage1(25)
         eng.load_gate(None)
         load_tables(eng, bs32, gpl)

@@ -172,7 +172,8 @@ def tables_k4():
 def test_k4_full_geometry_candidates_match_oracle(tables_k4, ora):
     """Config C (-k 4, default -n): 2^24 baby steps, 57.5 MiB level-1 bloom.  Every candidate of two
     whole chunks (2 x 1024 groups) equals the oracle's, and the key comes back through the second
-    check at k = 4 (M3 = 16384)."""
+    check at k = 4 (M3 = 16384).  The level-0 gate's candidates are the same with and without its
+    stage-1 fold (khb_set_gate_stage1), a subset of the ungated ones, and still hold the key."""
     from keyhuntm1cpu_amd.khbsgs import Engine
     bs = ora.Bsgs(None, 4)
     assert bs.m == tables_k4.m == 1 << 24 and bs.cycles == tables_k4.cycles == 1024
@@ -187,6 +188,17 @@ def test_k4_full_geometry_candidates_match_oracle(tables_k4, ora):
         e.load_lane_offsets(offs, gpl)
         centres = b"".join(tables_k4.chunk_centre(b, t.be64()) for b in bases)
         got, degen, st = e.scan(centres, 0, tables_k4.cycles)
+        # the product gate at k = 4 (2^30 bits, 128 MiB) with and without its 32 MiB stage-1 fold
+        gate, lg = tables_k4.gate()
+        gated = {}
+        for stage1 in (0, 25):
+            e.set_gate_stage1(stage1)
+            e.load_gate(gate, lg, tables_k4.gate_probes())
+            gated[stage1], gdegen, _ = e.scan(centres, 0, tables_k4.cycles)
+            assert not gdegen
+    assert sorted(gated[25]) == sorted(gated[0])
+    assert set(gated[0]) <= set(got)
+    assert any(tables_k4.secondcheck(bases[0], a, t.be64()) == key for jj, a in gated[25] if jj == 0)
     assert not degen
     for j, b in enumerate(bases):
         ref, _, _ = bs.scan(bs.chunk_start(b, t), 0, bs.cycles)
