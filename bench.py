@@ -63,12 +63,13 @@ def cpu_baseline(seconds: float, threads: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # default: >= 30 s of steady state — 600 steps x 2^31 giant steps at ~54 ms
-    ap.add_argument("--steps", type=int, default=600)
+    # default: >= 30 s of steady state — 320 steps x 2^32 giant steps at ~98 ms
+    ap.add_argument("--steps", type=int, default=320)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--chunks", type=int, default=0,
-                    help="chunks (2N keys each) per step; default: the fewest chunks that give every lane of "
-                         "the device one work item (512 at k=1, 2048 at k=4), at least 2^30 giant steps")
+                    help="chunks (2N keys each) per step; default: the chunks that give every lane of the device "
+                         "two work items (1024 at k=1, 4096 at k=4), as the CLI's auto batch does "
+                         "(engine.cpp batch_chunks)")
     ap.add_argument("--k", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -94,7 +95,9 @@ def main():
         # >= 2^30 giant steps per step, and enough work items to give every lane one
         from keyhuntm1cpu_amd import khbsgs
         fill = -(-khbsgs.default_lanes(local) * khbsgs.groups_per_item() // tables.cycles)
-        args.chunks = max(1, (1 << 30) // (tables.cycles * 1024), fill)
+        # two work items per lane, as the CLI's auto batch (engine.cpp batch_chunks): the launch's
+        # ramp and tail are paid once per 2 items (+1 % vs one item, profiles/r01b_batch_size.txt)
+        args.chunks = max(1, (1 << 30) // (tables.cycles * 1024), 2 * fill)
     target = puzzle66_target()
     two_n = 2 * (tables.n_low)                     # 2N keys per chunk
     key_chunk = (PUZZLE66_KEY - (1 << 65)) // two_n
