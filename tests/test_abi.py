@@ -49,3 +49,12 @@ def test_strerror():
     lib.khb_strerror.restype = C.c_char_p
     assert lib.khb_strerror(0) == b"ok"
     assert b"gfx950" in lib.khb_strerror(-2)
+
+
+def test_null_context_is_einval():
+    """Entry points that take a context reject a null one with KHB_EINVAL (-1) before any HIP call."""
+    lib = C.CDLL(os.path.join(LIB_DIR, "libkhbsgs.so"))
+    lib.khb_set_gate_stage1.argtypes = [C.c_void_p, C.c_uint32]
+    lib.khb_load_gate.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32]
+    assert lib.khb_set_gate_stage1(None, 25) == -1
+    assert lib.khb_load_gate(None, None, 0, 1) == -1
