@@ -102,3 +102,6 @@ $(LIBDIR)/variants/libkhbsgs_nonop.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 $(LIBDIR)/variants/libkhbsgs_h%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) -DKHB_GATE1=$* -shared -o $@ $(CSRC)/khbsgs.hip
+$(LIBDIR)/variants/libkhbsgs_gnt%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_GATE_NT=$* -shared -o $@ $(CSRC)/khbsgs.hip

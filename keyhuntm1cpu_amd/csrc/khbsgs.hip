@@ -263,8 +263,16 @@ struct GatePend {
   __device__ __forceinline__ bool pass() const { return gate_block_pass(lo, hi, bits); }
 };
 
+#ifndef KHB_GATE_NT
+#define KHB_GATE_NT 0             // 1 = gate blocks through non-temporal loads (experiment)
+#endif
 __device__ __forceinline__ GatePend gate_issue(const ScanArgs& A, const Fe& x) {
+#if KHB_GATE_NT
+  const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(A.gate) + (x.v[0] & A.gate_mask));
+  const uint2 w = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+#else
   const uint2 w = reinterpret_cast<const uint2*>(A.gate)[x.v[0] & A.gate_mask];
+#endif
   return GatePend{w.x, w.y, gate_bits(A, x)};
 }
 
