@@ -37,6 +37,18 @@ def test_puzzle30_known_answer():
     assert res == [0x3D94CD64]
 
 
+def test_last_chunk_overruns_range_end():
+    """a chunk is claimed while its base is below the range end
+    (keyhunt.cpp:3843-3844) and then scanned whole, so a key past the end but inside the last
+    claimed chunk is found; one in the next chunk is not (the scan stops after one chunk)."""
+    t = khhost.Tables("0x100000", 1, threads=8)      # N = 2^20, one chunk = 2N = 2^21 keys
+    start = 1 << 40
+    inside, beyond = start + (1 << 21) - 1000, start + (1 << 21) + 1000
+    res, st = t.search([khhost.pubkey(inside), khhost.pubkey(beyond)], start, start + 1)
+    assert res == [inside, None]
+    assert st["chunks"] == 1
+
+
 @pytest.mark.parametrize("nexp", [20, 24, 28])
 def test_puzzles_multi_target(keys, nexp):
     """All puzzles whose range fits [2^(nexp+1), 2^(nexp+8)) in one multi-target run."""
