@@ -97,6 +97,35 @@ def test_full_geometry_candidates_match_oracle(tables_k1, ora):
     assert any(tables_k1.secondcheck(bases[0], a, t.be64()) == key for a in a_hits)
 
 
+def test_random_chunks_candidates_match_oracle(tables_k1, ora):
+    """Default -n (2^44), k=1: 12 jobs of seeded random (chunk base, target key) pairs over
+    [2^65, 2^66), scanned in one launch; every job's L1 candidates equal the oracle's."""
+    import random
+    from keyhuntm1cpu_amd.khbsgs import Engine
+    bs = ora.Bsgs(None, 1)
+    rng = random.Random(0x6B68)
+    two_n = 1 << 45
+    jobs = []
+    for _ in range(12):
+        base = (1 << 65) + rng.randrange(1 << 20) * two_n
+        jobs.append((base, ora.pubkey((1 << 65) + rng.randrange(1 << 65))))
+    with Engine(0) as e:
+        bf, nb, bits, h = tables_k1.bloom_concat(1)
+        e.load_bloom(bf, nb, bits, h)
+        e.load_giant_table(tables_k1.giant_table())
+        offs, gpl = tables_k1.lane_offsets()
+        e.load_lane_offsets(offs, gpl)
+        centres = b"".join(tables_k1.chunk_centre(b, t.be64()) for b, t in jobs)
+        got, degen, st = e.scan(centres, 0, tables_k1.cycles)
+    assert not degen
+    total = 0
+    for j, (b, t) in enumerate(jobs):
+        ref, _, _ = bs.scan(bs.chunk_start(b, t), 0, bs.cycles)
+        assert sorted(a for jj, a in got if jj == j) == sorted(ref), j
+        total += len(ref)
+    assert total > 12                          # ~4 L1 false positives per chunk (1e-6 x 2^22 steps)
+
+
 def test_full_geometry_gate(tables_k1, ora):
     """The product's level-0 gate on the real k=1 tables (2^28 bits, three bits per x in one 64-bit
     block): over two whole chunks the gated candidates are exactly the L1 candidates whose gate
