@@ -105,3 +105,6 @@ $(LIBDIR)/variants/libkhbsgs_h%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 $(LIBDIR)/variants/libkhbsgs_gnt%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) -DKHB_GATE_NT=$* -shared -o $@ $(CSRC)/khbsgs.hip
+$(LIBDIR)/variants/libkhbsgs_dyn%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_DYN=$* -shared -o $@ $(CSRC)/khbsgs.hip

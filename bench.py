@@ -63,12 +63,12 @@ def cpu_baseline(seconds: float, threads: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # default: >= 30 s of steady state — 320 steps x 2^32 giant steps at ~98 ms
-    ap.add_argument("--steps", type=int, default=320)
+    # default: >= 30 s of steady state — 100 steps x 2^34 giant steps at ~365 ms
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--chunks", type=int, default=0,
                     help="chunks (2N keys each) per step; default: the chunks that give every lane of the device "
-                         "two work items (1024 at k=1, 4096 at k=4), as the CLI's auto batch does "
+                         "eight work items (4096 at k=1, 16384 at k=4), as the CLI's auto batch does "
                          "(engine.cpp batch_chunks)")
     ap.add_argument("--k", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -80,6 +80,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch                                   # first: share torch's HIP runtime with our libraries
     import torch.distributed as dist
+    ndev = torch.cuda.device_count()
+    if ndev and local >= ndev:
+        # more ranks than visible GPUs (a multi-rank rehearsal on a smaller box): share round-robin
+        print(f"[bench] rank {rank}: LOCAL_RANK {local} >= {ndev} visible GPUs, using GPU {local % ndev}",
+              file=sys.stderr, flush=True)
+        local = local % ndev
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -95,9 +101,10 @@ def main():
         # >= 2^30 giant steps per step, and enough work items to give every lane one
         from keyhuntm1cpu_amd import khbsgs
         fill = -(-khbsgs.default_lanes(local) * khbsgs.groups_per_item() // tables.cycles)
-        # two work items per lane, as the CLI's auto batch (engine.cpp batch_chunks): the launch's
-        # ramp and tail are paid once per 2 items (+1 % vs one item, profiles/r01b_batch_size.txt)
-        args.chunks = max(1, (1 << 30) // (tables.cycles * 1024), 2 * fill)
+        # eight work items per lane, as the CLI's auto batch (engine.cpp batch_chunks): waves take
+        # items dynamically (KHB_DYN), so a deeper queue keeps every SIMD 4 waves deep until the
+        # launch's last items (profiles/r01c_dyn_probe.txt)
+        args.chunks = max(1, (1 << 30) // (tables.cycles * 1024), 8 * fill)
     target = puzzle66_target()
     two_n = 2 * (tables.n_low)                     # 2N keys per chunk
     key_chunk = (PUZZLE66_KEY - (1 << 65)) // two_n

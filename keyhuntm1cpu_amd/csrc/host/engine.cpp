@@ -147,7 +147,9 @@ uint32_t batch_chunks(const Tables& T, const SearchConfig& cfg, size_t ntargets,
   const uint64_t per_item = khb_groups_per_item();
   const uint64_t lanes_per_job = (T.geo.cycles + per_item - 1) / per_item;
   const uint64_t lanes = ctx_lanes ? ctx_lanes : 256u * 16u * 64u;
-  const uint64_t jobs = (2ull * lanes + lanes_per_job - 1) / lanes_per_job;    // ~2 work items per lane
+  // ~8 work items per lane: the kernel's waves take items dynamically (KHB_DYN), so a deep queue
+  // keeps the device full until the batch's last items
+  const uint64_t jobs = (8ull * lanes + lanes_per_job - 1) / lanes_per_job;
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(jobs / std::max<size_t>(1, ntargets), 65536));
 }
 

@@ -56,6 +56,9 @@ struct AffPt {
 #ifndef KHB_GATE1
 #define KHB_GATE1 25              // default log2 bytes of the stage-1 fold of a larger level-0 gate (0 = none)
 #endif
+#ifndef KHB_DYN
+#define KHB_DYN 1                 // scan_batch kernels: dynamic per-wave work items (launch counter)
+#endif
 #ifndef KHB_WAVES_PER_SIMD
 #define KHB_WAVES_PER_SIMD 4      // occupancy target of k_giant_scan (launch bounds); w4 measured best
 #endif
@@ -986,6 +989,27 @@ __global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanA
 #endif
   if (QUEUE) *Q.n = 0;
   if constexpr (BATCH) {
+#if KHB_DYN
+    // Dynamic work items: each wave takes the next 64 items from a launch-wide counter
+    // (counters[2], zeroed per launch), so a wave that runs ahead keeps taking work and every SIMD
+    // stays 4 waves deep until the queue is empty; a static lane-strided split left the launch's
+    // tail to its slowest waves.  Each lane keeps its own scratch column (scr) for every item.
+    const uint32_t wl = threadIdx.x & 63u;
+    for (;;) {
+      uint32_t b = 0;
+      if (wl == 0) b = atomicAdd(&A.counters[2], 64u);
+      b = __builtin_amdgcn_readfirstlane(b);
+      if (b >= A.n_items) break;
+      const uint64_t item = (uint64_t)b + wl;
+      if (item < A.n_items) {
+        const uint32_t job = (uint32_t)(item / A.lanes_per_job);
+        const uint32_t m = (uint32_t)(item % A.lanes_per_job);
+        const uint32_t g0 = A.group_begin + m * kBatch;
+        const uint32_t g1 = min(g0 + kBatch, A.group_end);
+        scan_batch<MODE>(A, Q, job, g0, g1, scr);
+      }
+    }
+#else
     for (uint64_t item = lane; item < A.n_items; item += A.stride) {
       const uint32_t job = (uint32_t)(item / A.lanes_per_job);
       const uint32_t m = (uint32_t)(item % A.lanes_per_job);
@@ -993,6 +1017,7 @@ __global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanA
       const uint32_t g1 = min(g0 + kBatch, A.group_end);
       scan_batch<MODE>(A, Q, job, g0, g1, scr);
     }
+#endif
   } else {
     for (uint64_t item = lane; item < A.n_items; item += A.stride) {
       const uint32_t job = (uint32_t)(item / A.lanes_per_job);
@@ -1375,6 +1400,7 @@ int khb_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t gro
   KHB_TRY(c, hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, c->stream));
   KHB_TRY(c, hipMemsetAsync(c->d_counters, 0, 16, c->stream));
   ScanArgs A = make_args(c, n_jobs, group_begin, group_count, kBatch);
+  if (A.n_items > 0xFFFFFF00ull) return KHB_EINVAL;      // the 32-bit work-item counter (KHB_DYN)
   const uint32_t blocks = c->lanes / kBlock;
   KHB_TRY(c, hipEventRecord(c->ev0, c->stream));
   if (c->d_gate1)
