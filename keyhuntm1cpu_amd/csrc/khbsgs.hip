@@ -1019,7 +1019,19 @@ __global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanA
     }
 #endif
   } else {
+#if KHB_DYN
+    // dynamic per-wave items, as above (counters[2])
+    const uint32_t wl = threadIdx.x & 63u;
+    for (;;) {
+      uint32_t b = 0;
+      if (wl == 0) b = atomicAdd(&A.counters[2], 64u);
+      b = __builtin_amdgcn_readfirstlane(b);
+      if (b >= A.n_items) break;
+      const uint64_t item = (uint64_t)b + wl;
+      if (item >= A.n_items) continue;
+#else
     for (uint64_t item = lane; item < A.n_items; item += A.stride) {
+#endif
       const uint32_t job = (uint32_t)(item / A.lanes_per_job);
       const uint32_t m = (uint32_t)(item % A.lanes_per_job);
       const uint32_t g0 = A.group_begin + m * A.gpl;
