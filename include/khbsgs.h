@@ -35,6 +35,8 @@ extern "C" {
 #define KHB_EHIP -4       /* HIP runtime error (khb_last_hip_error() has the hipError_t) */
 #define KHB_ESTATE -5     /* call order violated (e.g. scan before tables are loaded) */
 #define KHB_EBUSY -6      /* a submission is still in flight */
+#define KHB_EINCOMPLETE -7 /* collect: the groups the kernel counted as walked differ from the submitted
+                             n_jobs x group_count (a work-item bookkeeping fault; results incomplete) */
 
 #define KHB_GROUP 1024         /* giant steps per group: CPU_GRP_SIZE, keyhunt.cpp:127 */
 #define KHB_GIANT_TABLE 513    /* GSn[0..511] + _2GSn, keyhunt.cpp:1318-1338 */
@@ -57,7 +59,7 @@ typedef struct {
 typedef struct {
   uint32_t n_cand;         /* total hits (may exceed the capacity given to khb_collect) */
   uint32_t n_degenerate;
-  uint64_t giant_steps;    /* giant steps scanned by the submission */
+  uint64_t giant_steps;    /* giant steps the device walked (counted on the device: groups x 1024) */
   float kernel_ms;         /* device time of the scan kernel (HIP events on the ctx stream) */
 } khb_stats;
 

@@ -89,6 +89,7 @@ constexpr uint32_t kHalf = KHB_GROUP / 2;            // 512
 constexpr uint32_t kCandCap = 1u << 20;
 constexpr uint32_t kAddrHitCap = 1u << 18;
 constexpr uint32_t kDegenCap = 4096;
+constexpr size_t kCounterBytes = 32;                 // ScanArgs::counters
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
@@ -123,7 +124,8 @@ struct ScanArgs {
   Fe* __restrict__ scratch;            // prefix products [512][lanes]
   khb_cand* __restrict__ cand;
   khb_degenerate* __restrict__ degen;
-  uint32_t* __restrict__ counters;     // [0] candidates [1] degenerate groups
+  uint32_t* __restrict__ counters;     // [0] candidates [1] degenerate groups [2] work-item cursor (KHB_DYN)
+                                       // [4..5] groups walked (u64, count_walked)
   uint8_t* __restrict__ xdump;         // dump modes only
   uint32_t* __restrict__ ahits;        // -m address hits: {job, group, t, kind} x ahit_cap
   uint32_t ahit_cap;
@@ -803,8 +805,8 @@ __device__ __forceinline__ Fe fe_small(uint32_t v) {
 // g*512 + 511 = T_g then inv(T_g); kBatch*512 + 2g (+1) = C_g.x (.y); kBatch*514 + g = chained
 // products.
 template <int MODE>
-__device__ __forceinline__ void scan_batch(const ScanArgs& A, ProbeQueue& Q, uint32_t job, uint32_t g0, uint32_t g1,
-                                           Fe* scr) {
+__device__ __forceinline__ uint32_t scan_batch(const ScanArgs& A, ProbeQueue& Q, uint32_t job, uint32_t g0,
+                                               uint32_t g1, Fe* scr) {
   const size_t S = A.stride;
   const GsnTable gsn{A.gsn};
   const uint32_t nb = g1 - g0;
@@ -917,7 +919,8 @@ __device__ __forceinline__ void scan_batch(const ScanArgs& A, ProbeQueue& Q, uin
     sg[(kHalf - 1) * S] = ig;
   }
   // 3. backward walks
-  for (uint32_t g = 0; g < nb; ++g) {
+  uint32_t walked = 0;
+  for (uint32_t g = 0; g < nb; ++g, ++walked) {
     Fe* const sg = scr + (size_t)g * kHalf * S;
     asm volatile("" ::: "memory");
     const AffPt C{sc[2 * g * S], sc[(2 * g + 1) * S]};
@@ -930,6 +933,7 @@ __device__ __forceinline__ void scan_batch(const ScanArgs& A, ProbeQueue& Q, uin
       if (k < A.degen_cap) A.degen[k] = khb_degenerate{job, g0 + g};
     }
   }
+  return walked;
 }
 
 // Per-group centre offsets gofs[j] = j*_2GSn from lane offsets offs[m] = (m*gpl)*_2GSn:
@@ -973,6 +977,17 @@ __global__ void k_expand_offsets(const AffPt* __restrict__ offs, uint32_t gpl, c
   out[j] = p;
 }
 
+// Groups walked by the launch: a wave sum of every lane's count, one 64-bit atomic per wave into
+// counters[4..5].  The host compares it with n_jobs x group_count (khb_collect: KHB_EINCOMPLETE), so
+// a work-item handout that skipped or repeated a group cannot go unnoticed.  Called with the wave
+// reconverged (after the item loop).
+__device__ __forceinline__ void count_walked(uint32_t* counters, uint32_t walked) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) walked += __shfl_xor(walked, o);
+  if ((threadIdx.x & 63u) == 0 && walked)
+    atomicAdd(reinterpret_cast<unsigned long long*>(counters + 4), (unsigned long long)walked);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanArgs A) {
   constexpr bool QUEUE = is_scan(MODE);
@@ -988,6 +1003,7 @@ __global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanA
   ProbeQueue Q{s_queue[wave], &s_count[wave]};
 #endif
   if (QUEUE) *Q.n = 0;
+  uint32_t walked = 0;     // groups this lane walked (count_walked: the host checks the launch's total)
   if constexpr (BATCH) {
 #if KHB_DYN
     // Dynamic work items: each wave takes the next 64 items from a launch-wide counter
@@ -1006,7 +1022,7 @@ __global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanA
         const uint32_t m = (uint32_t)(item % A.lanes_per_job);
         const uint32_t g0 = A.group_begin + m * kBatch;
         const uint32_t g1 = min(g0 + kBatch, A.group_end);
-        scan_batch<MODE>(A, Q, job, g0, g1, scr);
+        walked += scan_batch<MODE>(A, Q, job, g0, g1, scr);
       }
     }
 #else
@@ -1015,7 +1031,7 @@ __global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanA
       const uint32_t m = (uint32_t)(item % A.lanes_per_job);
       const uint32_t g0 = A.group_begin + m * kBatch;
       const uint32_t g1 = min(g0 + kBatch, A.group_end);
-      scan_batch<MODE>(A, Q, job, g0, g1, scr);
+      walked += scan_batch<MODE>(A, Q, job, g0, g1, scr);
     }
 #endif
   } else {
@@ -1044,10 +1060,11 @@ __global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanA
           if (k < A.degen_cap) A.degen[k] = khb_degenerate{job, g0 | 0x80000000u};
         }
       }
-      for (uint32_t j = g0; j < g1; ++j) scan_group<MODE>(A, Q, C, job, j, scr);
+      for (uint32_t j = g0; j < g1; ++j, ++walked) scan_group<MODE>(A, Q, C, job, j, scr);
     }
   }
   if (QUEUE) q_drain(A, Q, 1);   // the wave has reconverged: finish what is still queued
+  count_walked(A.counters, walked);
 }
 
 // hash160 self-test: for x||y points, kind 0/1 = compressed with prefix 02/03, 2 = uncompressed;
@@ -1144,6 +1161,13 @@ void pts_from_be(AffPt* dst, const uint8_t* src, uint32_t n) {
   }
 }
 
+// Groups the last launch walked (count_walked, copied back with the counters).
+uint64_t walked_groups(const khb_ctx* c) {
+  uint64_t v;
+  memcpy(&v, c->h_counters + 4, sizeof v);
+  return v;
+}
+
 int ensure_centres(khb_ctx* c, uint32_t n) {
   if (n <= c->centres_cap) return KHB_OK;
   if (c->d_centres) hipFree(c->d_centres);
@@ -1232,6 +1256,7 @@ const char* khb_strerror(int code) {
     case KHB_EHIP: return "HIP runtime error";
     case KHB_ESTATE: return "call order violated (tables not loaded?)";
     case KHB_EBUSY: return "submission in flight";
+    case KHB_EINCOMPLETE: return "the device walked a different number of groups than submitted";
     default: return "unknown error";
   }
 }
@@ -1280,8 +1305,8 @@ int khb_open(int device, uint32_t lanes, khb_ctx** out) {
   if ((e = hipMalloc(&c->d_scratch, sizeof(Fe) * kScratchEntries * lanes)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&c->d_cand, sizeof(khb_cand) * kCandCap)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&c->d_degen, sizeof(khb_degenerate) * kDegenCap)) != hipSuccess) return fail(e);
-  if ((e = hipMalloc(&c->d_counters, 16)) != hipSuccess) return fail(e);
-  if ((e = hipHostMalloc((void**)&c->h_counters, 16, hipHostMallocDefault)) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&c->d_counters, kCounterBytes)) != hipSuccess) return fail(e);
+  if ((e = hipHostMalloc((void**)&c->h_counters, kCounterBytes, hipHostMallocDefault)) != hipSuccess) return fail(e);
   if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return fail(e);
   if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return fail(e);
   *out = c;
@@ -1410,7 +1435,7 @@ int khb_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t gro
   if ((rc = ensure_centres(c, n_jobs)) || (rc = ensure_gofs(c))) return rc;
   pts_from_be(c->h_centres, centres, n_jobs);
   KHB_TRY(c, hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, c->stream));
-  KHB_TRY(c, hipMemsetAsync(c->d_counters, 0, 16, c->stream));
+  KHB_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounterBytes, c->stream));
   ScanArgs A = make_args(c, n_jobs, group_begin, group_count, kBatch);
   if (A.n_items > 0xFFFFFF00ull) return KHB_EINVAL;      // the 32-bit work-item counter (KHB_DYN)
   const uint32_t blocks = c->lanes / kBlock;
@@ -1423,7 +1448,7 @@ int khb_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t gro
     hipLaunchKernelGGL(k_giant_scan<kScan>, dim3(blocks), dim3(kBlock), 0, c->stream, A);
   KHB_TRY(c, hipGetLastError());
   KHB_TRY(c, hipEventRecord(c->ev1, c->stream));
-  KHB_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, 16, hipMemcpyDeviceToHost, c->stream));
+  KHB_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, kCounterBytes, hipMemcpyDeviceToHost, c->stream));
   c->in_flight = true;
   c->pending_steps = (uint64_t)n_jobs * group_count * KHB_GROUP;
   return KHB_OK;
@@ -1442,15 +1467,16 @@ int khb_collect(khb_ctx* c, khb_cand* cand, uint32_t cap, khb_degenerate* degen,
   uint32_t dt = nd < kDegenCap ? nd : kDegenCap;
   if (dt > degen_cap) dt = degen_cap;
   if (dt && degen) KHB_TRY(c, hipMemcpy(degen, c->d_degen, sizeof(khb_degenerate) * dt, hipMemcpyDeviceToHost));
+  const uint64_t steps = walked_groups(c) * KHB_GROUP;
   if (st) {
     st->n_cand = nc;
     st->n_degenerate = nd;
-    st->giant_steps = c->pending_steps;
+    st->giant_steps = steps;
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) ms = -1.f;
     st->kernel_ms = ms;
   }
-  return KHB_OK;
+  return steps == c->pending_steps ? KHB_OK : KHB_EINCOMPLETE;
 }
 
 int khb_scan(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count,
@@ -1472,7 +1498,7 @@ int khb_dump_x(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint32_t
   uint8_t* d_x = nullptr;
   KHB_TRY(c, hipMalloc(&d_x, bytes));
   hipError_t e = hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt), hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, 16, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, kCounterBytes, c->stream);
   if (e == hipSuccess) {
     ScanArgs A = make_args(c, 1, group_begin, group_count, kBatch);
     A.xdump = d_x;
@@ -1569,7 +1595,7 @@ int khb_addr_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_
   if ((rc = ensure_centres(c, n_jobs))) return rc;
   pts_from_be(c->h_centres, centres, n_jobs);
   KHB_TRY(c, hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, c->stream));
-  KHB_TRY(c, hipMemsetAsync(c->d_counters, 0, 16, c->stream));
+  KHB_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounterBytes, c->stream));
   ScanArgs A = make_args(c, n_jobs, group_begin, group_count);
   A.bloom = c->d_abloom;
   A.geom = c->ageom;
@@ -1584,7 +1610,7 @@ int khb_addr_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_
   }
   KHB_TRY(c, hipGetLastError());
   KHB_TRY(c, hipEventRecord(c->ev1, c->stream));
-  KHB_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, 16, hipMemcpyDeviceToHost, c->stream));
+  KHB_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, kCounterBytes, hipMemcpyDeviceToHost, c->stream));
   c->addr_in_flight = true;
   c->pending_steps = (uint64_t)n_jobs * group_count * KHB_GROUP;
   return KHB_OK;
@@ -1600,15 +1626,16 @@ int khb_addr_collect(khb_ctx* c, khb_addr_hit* hits, uint32_t cap, khb_stats* st
   uint32_t take = nh < kAddrHitCap ? nh : kAddrHitCap;
   if (take > cap) take = cap;
   if (take && hits) KHB_TRY(c, hipMemcpy(hits, c->d_ahits, sizeof(khb_addr_hit) * take, hipMemcpyDeviceToHost));
+  const uint64_t steps = walked_groups(c) * KHB_GROUP;
   if (st) {
     st->n_cand = nh;
     st->n_degenerate = nd;
-    st->giant_steps = c->pending_steps;
+    st->giant_steps = steps;
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) ms = -1.f;
     st->kernel_ms = ms;
   }
-  return KHB_OK;
+  return steps == c->pending_steps ? KHB_OK : KHB_EINCOMPLETE;
 }
 
 int khb_addr_scan(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count,
@@ -1630,7 +1657,7 @@ int khb_addr_dump(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint3
   uint8_t* d_xy = nullptr;
   KHB_TRY(c, hipMalloc(&d_xy, bytes));
   hipError_t e = hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt), hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, 16, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, kCounterBytes, c->stream);
   if (e == hipSuccess) {
     ScanArgs A = make_args(c, 1, group_begin, group_count);
     A.xdump = d_xy;
@@ -1729,7 +1756,7 @@ int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t
   }
   if (e == hipSuccess)
     e = hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, 16, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, kCounterBytes, c->stream);
   if (e == hipSuccess) e = hipEventRecord(c->ev0, c->stream);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_giant_scan<kBaby>, dim3(c->lanes / kBlock), dim3(kBlock), 0, c->stream, A);
@@ -1737,6 +1764,9 @@ int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t
   }
   if (e == hipSuccess) e = hipEventRecord(c->ev1, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  uint64_t walked = 0;
+  if (e == hipSuccess) e = hipMemcpy(c->h_counters, c->d_counters, kCounterBytes, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) walked = walked_groups(c);
   if (e == hipSuccess && kernel_ms) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) ms = -1.f;
@@ -1758,7 +1788,7 @@ int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t
   hipFree(dbp);
   hipFree(dgate);
   if (e != hipSuccess) return hip_fail(c, e);
-  return KHB_OK;
+  return walked == (uint64_t)n_jobs * groups_per_job ? KHB_OK : KHB_EINCOMPLETE;
 }
 
 }  // extern "C"

@@ -171,3 +171,36 @@ def test_cli_rmd160_compress_range(tmp_path, keys):
     assert r.returncode == 0, r.stderr
     assert f"Hit! Private Key: {k:x}\n" in r.stdout
     assert "[+] Search compress only" in r.stdout
+
+
+@pytest.mark.parametrize("search", [0, 1, 2])
+def test_addr_unsolvedpuzzles_bloom_matches_oracle(eng, ora, search):
+    """Config E's own target file (tests/unsolvedpuzzles.rmd, sized by keyhunt.cpp:6559-6576 with its
+    10,000-entry minimum): the bloom hit set of 64 groups equals the oracle's, first with the file
+    alone (three windows: the puzzle-71 range start, a random 2^70 key, a key near n), then with 200
+    planted hash160s of keys in a window appended to the file (keyhunt.cpp:2713-2735 checks)."""
+    text = _text("unsolvedpuzzles.rmd")
+    O = ora.AddrTable(text)
+    A = khhost.Addr(text, n_seq=1024 * 64, gpl=4)
+    assert A.table() and len(A.table()) == O.n
+    _load(eng, A)
+    gen = ora.AddrGen(1)
+    for base in (1 << 70, 0x3A5F0C2D9E8B7164F3 + search, N - 1024 * 64 - 7):
+        ref_hits, _ = _oracle_groups(ora, O, gen, base, 64, search)
+        hits, st = eng.addr_scan(khhost.pubkey(base + 512), 0, 64, search)
+        assert st.giant_steps == 1024 * 64
+        assert sorted((g, t, kind) for _, g, t, kind in hits) == ref_hits
+    rng = random.Random(100 + search)
+    base = (1 << 70) + 0x5151
+    picks = rng.sample(range(base, base + 1024 * 64), 200)
+    extra = [ora.pub_hash160(ora.pubkey(k), i % 2 == 0).hex() for i, k in enumerate(picks)]
+    text2 = text.rstrip("\n") + "\n" + "\n".join(extra) + "\n"
+    O2 = ora.AddrTable(text2)
+    A2 = khhost.Addr(text2, n_seq=1024 * 64, gpl=4)
+    _load(eng, A2)
+    ref_hits, ref_keys = _oracle_groups(ora, O2, gen, base, 64, search)
+    hits, _ = eng.addr_scan(khhost.pubkey(base + 512), 0, 64, search)
+    assert sorted((g, t, kind) for _, g, t, kind in hits) == ref_hits
+    assert len(ref_hits) >= 90
+    found, _ = A2.search(base, base + 1024 * 64, search=search, lanes=16384)
+    assert sorted(k for k, _, _ in found) == sorted(ref_keys)

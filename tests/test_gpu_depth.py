@@ -1,0 +1,84 @@
+"""GPU completeness at the product batch depth (keyhunt.cpp:3867-4004 run over a whole CLI batch).
+
+The product launches the CLI's auto batch: about eight work items per lane of a full residency,
+handed out dynamically per wave from a launch-wide counter (KHB_DYN).  The oracle-parity tests run
+fewer jobs than lanes, so they never see a wave come back for its second item.  Here one batch of
+that depth is searched through the product session with keys planted in the first job, a middle job
+and the ragged last group of the last job, on a geometry whose groups per chunk (342) is not a
+multiple of the 8 groups per item and whose item count is not a multiple of 64.  Every key must be
+found, and the giant steps the device counted (count_walked) must equal jobs x cycles x 1024.
+"""
+from __future__ import annotations
+
+import pytest
+
+from keyhuntm1cpu_amd import khbsgs, khhost
+
+pytestmark = pytest.mark.gpu
+
+N_STR, KF = "0x10000000000", 3          # M = 3 * 2^20, aux = 349525, cycles = 342 (keyhunt.cpp:3810-3813)
+
+
+def _auto_chunks(cycles: int, lanes: int, ntargets: int) -> int:
+    """engine.cpp batch_chunks: ceil(8 * lanes / items per job) jobs, split over the targets."""
+    per_job = -(-cycles // khbsgs.groups_per_item())
+    jobs = -(-8 * lanes // per_job)
+    return max(1, min(jobs // ntargets, 65536))
+
+
+def _planted(base: int, m: int, a: int) -> int:
+    """A key whose first giant-step hit in the chunk at `base` is step a: the key sits in the window
+    [base + 2M a, base + 2M (a + 1)) that secondcheck rebuilds (keyhunt.cpp:4271-4296)."""
+    return base + 2 * m * a + m // 2 + 17
+
+
+def test_batch_depth_completeness():
+    t = khhost.Tables(N_STR, KF, threads=16)
+    assert t.cycles == 342 and t.m == 3 << 20
+    lanes = khbsgs.default_lanes(0)
+    assert lanes > 0
+    nt = 3
+    chunks = _auto_chunks(t.cycles, lanes, nt)
+    per_job = -(-t.cycles // khbsgs.groups_per_item())
+    n_items = chunks * nt * per_job
+    assert n_items >= 8 * lanes - 64 * per_job * nt      # at least ~8 items per lane
+    assert n_items % 64 != 0                             # the last wave's item block is ragged
+    two_n = 2 * t.n_low
+    start = 1 << 52
+    bases = [start + c * two_n for c in range(chunks)]
+    mid = chunks // 2
+    last_a = t.cycles * 1024 - 1                         # last step of the ragged last group
+    keys = [
+        _planted(bases[0], t.m, 0),                      # first job, first giant step
+        _planted(bases[mid], t.m, 1024 * 171 + 500),     # a middle job, a middle work item
+        _planted(bases[-1], t.m, last_a),                # last job, ragged last item, last step
+    ]
+    # the last key lies beyond the last chunk's 2N keys (cycles * 1024 > aux), i.e. inside the next
+    # chunk's range, which this batch does not claim: only the last group of the last job reaches it
+    assert keys[2] >= bases[-1] + two_n
+    targets = [khhost.pubkey(k) for k in keys]
+    with khhost.Session(t, devices=[0]) as s:
+        res, st = s.run(targets, start, start + (chunks + 8) * two_n, max_chunks=chunks)
+    assert st["launches"] == 1 and st["chunks"] == chunks
+    assert st["giant_steps"] == chunks * nt * t.cycles * 1024     # counted on the device
+    assert res == keys
+    t.close()
+
+
+def test_device_step_count_matches_submission():
+    """khb_collect reports the device-counted giant steps for ragged shapes (one job; a job count
+    that leaves most lanes idle; a group range starting past group 0)."""
+    from keyhuntm1cpu_amd.khbsgs import Engine
+    t = khhost.Tables(N_STR, KF, threads=8)
+    tgt = khhost.pubkey(0x1234567890ABCDEF)
+    with Engine(0) as e:
+        bf, nb, bits, h = t.bloom_concat(1)
+        e.load_bloom(bf, nb, bits, h)
+        e.load_giant_table(t.giant_table())
+        offs, gpl = t.lane_offsets()
+        e.load_lane_offsets(offs, gpl)
+        for n_jobs, g0, gc in ((1, 0, 342), (37, 0, 342), (5, 8, 14), (3, 336, 6)):
+            centres = b"".join(t.chunk_centre((1 << 50) + i * 2 * t.n_low, tgt) for i in range(n_jobs))
+            _, _, st = e.scan(centres, g0, gc)
+            assert st.giant_steps == n_jobs * gc * 1024
+    t.close()
