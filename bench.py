@@ -1,19 +1,22 @@
 #!/usr/bin/env python3
-"""bench.py — BSGS giant-step throughput on puzzle #66 (BASELINE.json configs[1]: -b 66, k=1).
+"""bench.py — BSGS giant-step throughput (BASELINE.json metric) on puzzle #66 or puzzle #130.
 
-One step = one GPU scan batch of the product search (libkhhost -> libkhbsgs): host centres for
-512 chunks, the HIP giant-step kernel over all 4096 groups of each chunk (512 x 4096 x 1024 =
-2^31 giant steps: one 8-group work item per lane of a full residency; at k=4, 2048 chunks x 1024
-groups), and the CPU confirmation of every level-1 candidate, pipelined exactly as the keyhunt_amd
-CLI runs it.  Tables are built and resident in HBM
-before the timed region.  Chunks are sequential 2N-key chunks of -b 66 starting right after the
-chunk holding puzzle #66's (public) key, so the search never stops early on the find and every
-rank times exactly K steps.  Multi-GPU: one process per GPU (torch.distributed.run), rank r owns
-the r-th block of (W + K) x chunks consecutive chunks (weak scaling; no data-path collective:
-gloo only times it).  At N x K x chunks beyond -b 66's 2^20 chunks the blocks run on past 2^66;
-the work per giant step does not depend on the keys.
+--workload p66 (default; BASELINE.json configs[1], -b 66, k=1; --k 4 = configs[2]):
+  one step = one GPU scan batch of the product search (libkhhost -> libkhbsgs): host centres for
+  4096 chunks, the HIP giant-step kernel over all 4096 groups of each chunk (2^34 giant steps: eight
+  8-group work items per lane of a full residency, as the CLI's auto batch), and the CPU confirmation
+  of every candidate, pipelined exactly as the keyhunt_amd CLI runs it.  Chunks are sequential 2N-key
+  chunks of -b 66 starting right after the chunk holding puzzle #66's (public) key, so the search
+  never stops early and every rank times exactly K steps; rank r owns the r-th block of (W + K) x
+  chunks consecutive chunks (weak scaling).
+--workload p130 (BASELINE.json configs[3], -f tests/130.txt -b 130, k=1): the real #130 pubkey; the
+  whole -b 130 range [2^129, 2^130) is partitioned statically into one contiguous chunk block per
+  rank (partition.rank_range, north_star), and every rank scans (W + K) batches from its block start.
 
-Prints ONE JSON line (rank 0).  See DESIGN.md §Measurement for the roofline definitions.
+Tables are built and resident in HBM before the timed region.  Multi-GPU: one process per GPU
+(torch.distributed.run); no data-path collective (gloo only times it).
+
+Prints ONE JSON line (rank 0).  See DESIGN.md §5-§6 for the roofline definitions.
 """
 from __future__ import annotations
 
@@ -26,16 +29,26 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# Algorithmic work per giant step, counted in 32-bit
-# multiply-class lane ops of the reference algorithm: per 1024-step group 2561 field mul
-# (64 products + 8 fold) + 1023 field sqr (36 + 8) + one inversion (255 sqr + 15 mul), plus two
-# XXH64 of 32 bytes (22 64-bit multiplies = 66 32-bit) and two 64-bit "% bits" (4 each).
+# Algorithmic work per giant step, counted in 32-bit multiply-class
+# lane ops of the reference algorithm: per 1024-step group 2561 field mul (64 products + 8 fold) +
+# 1023 field sqr (36 + 8) + one inversion (255 sqr + 15 mul), plus two XXH64 of 32 bytes (22 64-bit
+# multiplies = 66 32-bit) and two 64-bit "% bits" (4 each).
 MUL_OPS, SQR_OPS = 72, 44
-OPS_PER_STEP = (2561 * MUL_OPS + 1023 * SQR_OPS + 255 * SQR_OPS + 15 * MUL_OPS) / 1024.0 + 2 * 66 + 2 * 4
-# Peak of the binding unit: v_mad_u64_u32 issue rate measured on MI355X by
-# tools/microbench/intops2.hip at full occupancy (profiles/r01_intops2.txt).
+INV_OPS = 255 * SQR_OPS + 15 * MUL_OPS
+OPS_PER_STEP = (2561 * MUL_OPS + 1023 * SQR_OPS + INV_OPS) / 1024.0 + 2 * 66 + 2 * 4
+# The multiply-class work this kernel executes per giant step: per group 511 forward
+# prefix products + the walk's 2045 products and 1023 squarings (walk_group_g) + 9 products and one
+# squaring of the work item's centre and chained-product bookkeeping (scan_batch), and two inversions
+# per 8-group work item; no XXH64 / "% bits" for the 99.96 % of x the level-0 gate stops.
+EXEC_OPS_PER_STEP = ((2556 + 9) * MUL_OPS + (1023 + 1) * SQR_OPS) / 1024.0 + 2 * INV_OPS / (8 * 1024.0)
+# Peak of the binding unit: v_mad_u64_u32 issue rate measured on MI355X by tools/microbench/intops2.hip
+# at full occupancy, 57.8 lane-ops/clk/CU at the 2.16 GHz the microbenchmark ran at
+# (profiles/r01_intops2.txt); the same rate at the 2.4 GHz peak engine clock is 35.5 T.
 PEAK_MULOPS_T = float(os.environ.get("KHB_PEAK_MULOPS_T", "32.04"))
+PEAK_CLK_GHZ, PEAK_LANES_PER_CLK_CU, CUS = 2.16, 57.8, 256
+PEAK_MULOPS_T_2P4 = round(PEAK_LANES_PER_CLK_CU * CUS * 2.4e9 / 1e12, 2)
 HBM_PEAK_GBS = 8000.0
+BSGSD_CPU_MKEYS = 16.9     # the reference's own published BSGS rate (BSGSD.md:52-58, 8 threads)
 
 PUZZLE66_KEY = 0x2832ED74F2B5E35EE            # public solution; pinned to tests/66.rmd below
 PUZZLE66_HASH160 = "20d45a6a762535700ce9e0b216e31994335db8a5"   # tests/66.rmd
@@ -50,12 +63,44 @@ def puzzle66_target():
     return xy
 
 
-def cpu_baseline(seconds: float, threads: int):
+def puzzle130_target():
+    """tests/130.txt of the reference (the committed fixture tests/golden/puzzle_targets.json)."""
+    from keyhuntm1cpu_amd import khhost
+    with open(os.path.join(REPO, "tests", "golden", "puzzle_targets.json")) as f:
+        line = json.load(f)["130.txt"][0]
+    xy, _ = khhost.parse_pubkey(line)
+    return xy, line
+
+
+def host_cores():
+    """Cores this job may use: the affinity set, capped by a cgroup v2 CPU quota and by the job's CPU
+    share when the environment states one (OMP_NUM_THREADS: a one-GPU box gives each job 16 of its
+    host's cores, while nproc shows the whole machine); plus nproc and the CPU model for the report."""
+    n = len(os.sched_getaffinity(0))
+    caps = {"affinity": n, "nproc": os.cpu_count()}
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        if q != "max":
+            caps["cgroup_quota"] = max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        pass
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        caps["job_share"] = int(os.environ["OMP_NUM_THREADS"])
+    cores = min(v for k, v in caps.items() if k != "nproc" and v)
+    try:
+        with open("/proc/cpuinfo") as f:
+            caps["cpu_model"] = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+    except OSError:
+        pass
+    return cores, caps
+
+
+def cpu_baseline(seconds: float, threads: int, target, base: int):
     """Oracle (plain-C restatement of thread_process_bsgs) on the host cores, same workload."""
     from oracle import ora
     bs = ora.Bsgs(None, 1, threads)
-    t = ora.pubkey(PUZZLE66_KEY)
-    steps, el = bs.bench(t, 1 << 65, threads, seconds)
+    steps, el = bs.bench(target, base, threads, seconds)
     bs.close()
     return steps / el
 
@@ -63,7 +108,9 @@ def cpu_baseline(seconds: float, threads: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # default: >= 30 s of steady state — 100 steps x 2^34 giant steps at ~365 ms
+    ap.add_argument("--workload", choices=("p66", "p130"), default="p66",
+                    help="p66: BASELINE configs[1] (-b 66; --k 4 = configs[2]); p130: configs[3] (-b 130)")
+    # default: >= 30 s of steady state — 100 steps x 2^34 giant steps at ~360 ms
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--chunks", type=int, default=0,
@@ -71,9 +118,12 @@ def main():
                          "eight work items (4096 at k=1, 16384 at k=4), as the CLI's auto batch does "
                          "(engine.cpp batch_chunks)")
     ap.add_argument("--k", type=int, default=1)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=60.0,
+                    help="CPU-baseline window (BASELINE.md: 60 s steady state after the table build)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if args.workload == "p130" and args.k != 1:
+        raise SystemExit("--workload p130 is BASELINE configs[3]: k = 1")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -98,19 +148,35 @@ def main():
     tables = khhost.Tables(None, args.k, threads=host_threads, gpl=4)
     t_build = time.time() - t0
     if not args.chunks:
-        # >= 2^30 giant steps per step, and enough work items to give every lane one
-        from keyhuntm1cpu_amd import khbsgs
-        fill = -(-khbsgs.default_lanes(local) * khbsgs.groups_per_item() // tables.cycles)
         # eight work items per lane, as the CLI's auto batch (engine.cpp batch_chunks): waves take
         # items dynamically (KHB_DYN), so a deeper queue keeps every SIMD 4 waves deep until the
         # launch's last items (profiles/r01c_dyn_probe.txt)
+        from keyhuntm1cpu_amd import khbsgs
+        fill = -(-khbsgs.default_lanes(local) * khbsgs.groups_per_item() // tables.cycles)
         args.chunks = max(1, (1 << 30) // (tables.cycles * 1024), 8 * fill)
-    target = puzzle66_target()
     two_n = 2 * (tables.n_low)                     # 2N keys per chunk
-    key_chunk = (PUZZLE66_KEY - (1 << 65)) // two_n
-    lo = (1 << 65) + (key_chunk + 1) * two_n      # -b 66, after the key's chunk
     per_rank = (args.warmup + args.steps) * args.chunks
-    start, end = rank_range(lo, lo + world * per_rank * two_n, two_n, rank, world)
+    if args.workload == "p66":
+        target = puzzle66_target()
+        key_chunk = (PUZZLE66_KEY - (1 << 65)) // two_n
+        lo = (1 << 65) + (key_chunk + 1) * two_n      # -b 66, after the key's chunk
+        start, end = rank_range(lo, lo + world * per_rank * two_n, two_n, rank, world)
+        cfg_idx = {1: "1", 4: "2"}.get(args.k, "1, k varied")
+        workload = "puzzle66 -m bsgs -b 66 -k %d (BASELINE configs[%s])" % (args.k, cfg_idx)
+        data = ("real puzzle #66 pubkey (solved key, hash160 == tests/66.rmd), -b 66 range, sequential chunks from "
+                "the chunk after the key's")
+        cpu_base = 1 << 65
+    else:
+        target, line = puzzle130_target()
+        lo, hi = 1 << 129, 1 << 130
+        start, end = rank_range(lo, hi, two_n, rank, world)      # the rank's static block of -b 130
+        if end - start < per_rank * two_n:
+            raise SystemExit("-b 130 block too small for the requested steps")
+        workload = "puzzle130 -m bsgs -f tests/130.txt -b 130 -k 1 (BASELINE configs[3])"
+        data = ("real puzzle #130 pubkey (tests/130.txt: %s...), -b 130 range [2^129, 2^130) split into %d static "
+                "contiguous chunk blocks, one per rank; each rank scans sequential chunks from its block start"
+                % (line[:16], world))
+        cpu_base = lo
     sess = khhost.Session(tables, devices=[local], chunks_per_batch=args.chunks, check_threads=host_threads)
 
     def sync():
@@ -130,7 +196,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     sess.close()
-    steps_done = st["giant_steps"]
+    steps_done = st["giant_steps"]               # counted on the device (khb_collect, count_walked)
     kernel_ms = 1e3 * st["kernel_s"] / max(1, st["launches"])
     tot_steps, tmax, kmax = steps_done, dt, kernel_ms
     if world > 1:
@@ -151,11 +217,22 @@ def main():
         print(f"[bench] WARNING: timed {tot_steps} giant steps, expected {world * args.steps * per_launch_steps}",
               file=sys.stderr, flush=True)
     achieved = OPS_PER_STEP * per_launch_steps / (kernel_ms * 1e-3) / 1e12
+    executed = EXEC_OPS_PER_STEP * per_launch_steps / (kernel_ms * 1e-3) / 1e12
     roofline = {"bound": "valu", "unit": "Tops/s", "achieved": round(achieved, 3), "peak": PEAK_MULOPS_T,
                 "frac": round(achieved / PEAK_MULOPS_T, 4), "traffic": None,
-                "ops": "32-bit multiply-class lane ops (v_mad_u64_u32 / v_mul_lo_u32)",
+                "ops": "32-bit multiply-class lane ops of the reference algorithm (v_mad_u64_u32 / v_mul_lo_u32)",
                 "ops_per_giant_step": round(OPS_PER_STEP, 2), "kernel": "k_giant_scan",
-                "kernel_ms_avg": round(kernel_ms, 3)}
+                "kernel_ms_avg": round(kernel_ms, 3),
+                "peak_basis": "v_mad_u64_u32 %.1f lane-ops/clk/CU x %d CUs at %.2f GHz (profiles/r01_intops2.txt); "
+                              "%.2f T at the 2.4 GHz peak clock" % (PEAK_LANES_PER_CLK_CU, CUS, PEAK_CLK_GHZ,
+                                                                    PEAK_MULOPS_T_2P4),
+                "frac_at_2p4ghz": round(achieved / PEAK_MULOPS_T_2P4, 4)}
+    executed_info = {"ops_per_giant_step": round(EXEC_OPS_PER_STEP, 2),
+                     "note": "multiply-class work the kernel performs: the reference's field work without the "
+                             "3 of 4 inversions the 8-group batch saves and without the two XXH64 the level-0 "
+                             "gate skips for 99.96 % of x",
+                     "achieved": round(executed, 3), "frac": round(executed / PEAK_MULOPS_T, 4),
+                     "frac_at_2p4ghz": round(executed / PEAK_MULOPS_T_2P4, 4)}
     pmc_path = os.path.join(REPO, "profiles", "pmc_latest.json")
     if os.path.exists(pmc_path):
         try:
@@ -164,15 +241,31 @@ def main():
             if pmc.get("chunks_per_launch") == args.chunks and pmc.get("k") == args.k:
                 roofline["traffic"] = pmc.get("hbm_bytes_per_launch")
                 roofline["traffic_source"] = os.path.relpath(pmc_path, REPO)
+                if pmc.get("valu_instr_per_giant_step"):
+                    vi = pmc["valu_instr_per_giant_step"]
+                    executed_info.update({
+                        "valu_lane_instr_per_giant_step": vi,
+                        "valu_busy_pct": pmc.get("valu_busy_pct"),
+                        "valu_lane_instr_T_per_s": round(vi * per_launch_steps / (kernel_ms * 1e-3) / 1e12, 2),
+                        "vop3_issue_ceiling": "58-61 lane-instr/clk/CU = %.1f-%.1f T at 2.4 GHz (intops2)"
+                                              % (58 * CUS * 2.4e-3, 61 * CUS * 2.4e-3),
+                        "pmc_source": pmc.get("valu_source")})
         except (OSError, ValueError):
             pass
+    roofline["executed"] = executed_info
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        c_threads = host_threads
-        v = cpu_baseline(args.cpu_seconds, c_threads)
+        c_threads, hinfo = host_cores()
+        from oracle import ora                     # the checker-side restatement, timed only here
+        cpu_pt = ora.pubkey(PUZZLE66_KEY) if args.workload == "p66" else ora.parse_pubkey(line)[0]
+        v = cpu_baseline(args.cpu_seconds, c_threads, cpu_pt, cpu_base)
         cpu = {"value": round(v / 1e6, 4), "unit": "Mkeys/s", "cores": c_threads, "kind": "port",
-               "sample": f"oracle thread_process_bsgs restatement, puzzle #66 target, chunks from 2^65, "
-                         f"{args.cpu_seconds:.0f} s window on {c_threads} threads (tables built first)"}
+               "sample": f"oracle thread_process_bsgs restatement (k=1, default -n), same target, chunks from "
+                         f"{hex(cpu_base)}, {args.cpu_seconds:.0f} s window on {c_threads} threads (all cores this job "
+                         f"may use) after the table build",
+               "host": hinfo,
+               "reference_published": {"value": BSGSD_CPU_MKEYS, "unit": "M giant-steps/s",
+                                       "source": "BSGSD.md:52-58 (bsgsd -k 4096 -t 8, unnamed 64 GB server)"}}
     out = {
         "metric": "Mkeys/s (BSGS giant-steps/s) on puzzle #66 at 1/2/4/8 MI355X",
         "value": round(gsps / 1e6, 2),
@@ -185,13 +278,12 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "real puzzle #66 pubkey (solved key, hash160 == tests/66.rmd), -b 66 range, sequential "
-                "chunks from the chunk after the key's",
-        "config": {"workload": "puzzle66 -m bsgs -b 66 -k %d (BASELINE configs[%s])"
-                               % (args.k, {1: "1", 4: "2"}.get(args.k, "1, k varied")),
+        "data": data,
+        "config": {"workload": workload,
                    "n": hex(tables.n_low), "bsgs_m": tables.m, "groups_per_chunk": tables.cycles,
                    "chunks_per_step": args.chunks, "giant_steps_per_step": per_launch_steps,
                    "parallelism": "range-partition x%d" % world, "table_build_s": round(t_build, 2),
+                   "rank0_range": [hex(start), hex(end)],
                    "ref_keys_per_s": "%.3e" % (gsps * 2 * tables.m),
                    "candidates": st["candidates"], "found": [hex(r) if r else None for r in res]},
         "roofline": roofline,
