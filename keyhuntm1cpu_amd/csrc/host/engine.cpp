@@ -1,10 +1,12 @@
 #include "engine.hpp"
 
+#include <stdlib.h>
 #include <string.h>
 #include <sys/random.h>
 
 #include <algorithm>
 #include <atomic>
+#include <deque>
 #include <mutex>
 #include <thread>
 
@@ -153,7 +155,10 @@ uint32_t batch_chunks(const Tables& T, const SearchConfig& cfg, size_t ntargets,
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(jobs / std::max<size_t>(1, ntargets), 65536));
 }
 
-// One device: claim/centre the next batch and confirm the previous one while the GPU scans.
+// One device: up to `queue_depth` batches queued on the GPU (khb_submit fills the context's next
+// slot, each on its own stream, so a queued batch takes over the CUs the running one's last waves
+// free); the next batch is claimed and centred while the GPU scans, and each collected batch is
+// confirmed after its successor has been submitted.
 void device_thread(Shared& S, khb_ctx* ctx) {
   auto fail = [&](int rc, const char* what) {
     std::lock_guard<std::mutex> lk(S.mu);
@@ -168,61 +173,71 @@ void device_thread(Shared& S, khb_ctx* ctx) {
   const uint32_t want = batch_chunks(T, S.cfg, S.targets.size(), khb_lanes(ctx));
   const int threads = S.cfg.check_threads > 0 ? S.cfg.check_threads
                                                : (int)std::max(2u, std::min(16u, std::thread::hardware_concurrency()));
+  const int depth = std::max(1, std::min(S.cfg.queue_depth, 2));
   std::vector<khb_cand> cbuf(1u << 20);
   std::vector<khb_degenerate> dbuf(4096);
-  Batch bat[3];
-  int cur = 0, nxt = 1, prv = 2;
-  std::vector<khb_cand> prev_cands;
-  bool have_prev = false;
+  std::vector<Batch> ring(depth + 1);
+  int next = 0;
+  auto take = [&]() { const int i = next; next = (next + 1) % (int)ring.size(); return i; };
   auto stopped = [&]() { std::lock_guard<std::mutex> lk(S.mu); return S.stop; };
   auto prepare = [&](Batch& b) {
     if (stopped() || !claim(S, want, b)) return false;
     make_jobs(S, b, threads);
     return !b.job_chunk.empty();
   };
-  bool have_cur = prepare(bat[cur]);
+  auto submit = [&](Batch& b) {
+    return khb_submit(ctx, b.centres.data(), (uint32_t)b.job_chunk.size(), 0, cycles);
+  };
+  std::deque<int> q;          // batches on the GPU, oldest first
   int rc = 0;
-  if (have_cur) {
-    rc = khb_submit(ctx, bat[cur].centres.data(), (uint32_t)bat[cur].job_chunk.size(), 0, cycles);
-    if (rc) { fail(rc, "khb_submit"); return; }
+  while ((int)q.size() < depth) {
+    const int i = take();
+    if (!prepare(ring[i])) break;
+    if ((rc = submit(ring[i]))) { fail(rc, "khb_submit"); break; }
+    q.push_back(i);
   }
-  while (have_cur) {
-    const bool have_next = prepare(bat[nxt]);                  // overlaps the GPU scan of cur
-    if (have_prev) confirm(S, bat[prv], prev_cands, threads);  // overlaps the GPU scan of cur
-    have_prev = false;
-    khb_stats st{};
-    rc = khb_collect(ctx, cbuf.data(), (uint32_t)cbuf.size(), dbuf.data(), (uint32_t)dbuf.size(), &st);
-    if (rc) { fail(rc, "khb_collect"); return; }
-    if (have_next) {
-      rc = khb_submit(ctx, bat[nxt].centres.data(), (uint32_t)bat[nxt].job_chunk.size(), 0, cycles);
-      if (rc) { fail(rc, "khb_submit"); return; }
+  int pre = -1;               // claimed and centred, not yet submitted
+  std::vector<khb_cand> cands;
+  while (!q.empty()) {
+    if (pre < 0 && !rc) {
+      const int k = take();
+      if (prepare(ring[k])) pre = k;                           // overlaps the GPU scan
     }
-    if (st.n_cand > cbuf.size()) { fail(KHB_ENOMEM, "candidate buffer overflow (lower the batch size)"); return; }
+    const int i = q.front();
+    q.pop_front();
+    khb_stats st{};
+    const int crc = khb_collect(ctx, cbuf.data(), (uint32_t)cbuf.size(), dbuf.data(), (uint32_t)dbuf.size(), &st);
+    if (crc) { fail(crc, "khb_collect"); rc = crc; continue; }  // keep draining the queue
+    if (pre >= 0 && !rc) {
+      if ((rc = submit(ring[pre]))) fail(rc, "khb_submit");
+      else q.push_back(pre);
+    }
+    pre = -1;
+    if (rc) continue;
+    if (st.n_cand > cbuf.size()) {
+      fail(KHB_ENOMEM, "candidate buffer overflow (lower the batch size)");
+      rc = KHB_ENOMEM;
+      continue;
+    }
+    const Batch& b = ring[i];
     {
       std::lock_guard<std::mutex> lk(S.mu);
       S.stats.launches += 1;
-      S.stats.chunks += bat[cur].bases.size();
+      S.stats.chunks += b.bases.size();
       S.stats.giant_steps += st.giant_steps;
       S.stats.candidates += st.n_cand;
       S.stats.degenerate += st.n_degenerate;
       S.stats.kernel_seconds += st.kernel_ms * 1e-3;
-      for (uint32_t i = 0; i < st.n_degenerate && i < dbuf.size(); ++i) {
+      for (uint32_t d = 0; d < st.n_degenerate && d < dbuf.size(); ++d) {
         if (!S.cb.on_warning) break;
-        const uint32_t job = dbuf[i].job;
+        const uint32_t job = dbuf[d].job;
         S.cb.on_warning("[W] collapsed batch inverse (target on a window centre): chunk 0x" +
-                        bat[cur].bases[bat[cur].job_chunk[job]].hex() + " group " +
-                        std::to_string(dbuf[i].group & 0x7fffffffu));
+                        b.bases[b.job_chunk[job]].hex() + " group " + std::to_string(dbuf[d].group & 0x7fffffffu));
       }
     }
-    prev_cands.assign(cbuf.begin(), cbuf.begin() + st.n_cand);
-    have_prev = true;
-    const int old_prv = prv;
-    prv = cur;
-    cur = nxt;
-    nxt = old_prv;
-    have_cur = have_next;
+    cands.assign(cbuf.begin(), cbuf.begin() + st.n_cand);
+    confirm(S, b, cands, threads);                             // overlaps the GPU scan of the queue
   }
-  if (have_prev) confirm(S, bat[prv], prev_cands, threads);
 }
 
 }  // namespace
@@ -268,6 +283,7 @@ int Session::run(const std::vector<Target>& targets, const U256& start, const U2
   SearchConfig cfg = cfg_;
   cfg.max_chunks = max_chunks;
   cfg.random_chunks = random_chunks;
+  if (const char* q = getenv("KHB_QUEUE_DEPTH")) cfg.queue_depth = atoi(q);   // A/B timing of the tail overlap
   Shared S(*T_, targets, cfg, cb, found, keys, stats);
   S.start = start;
   S.end = end;

@@ -29,6 +29,7 @@ struct SearchConfig {
   uint64_t max_chunks = 0;         // 0 = until range end
   bool random_chunks = false;      // -B random: every chunk base drawn uniformly in the range
   bool use_gate = true;            // load the tables' level-0 gate (khb_load_gate) when they have one
+  int queue_depth = 2;             // batches queued per device (1 or 2; 2 overlaps launch tails)
 };
 
 struct SearchStats {

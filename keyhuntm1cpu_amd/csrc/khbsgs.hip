@@ -1111,9 +1111,28 @@ __global__ void k_probe(const uint8_t* __restrict__ bloom, BloomGeom g, const Fe
 
 }  // namespace
 
+// One submission's device state.  A context owns two (KHB_QUEUE_DEPTH): khb_submit fills the next
+// free slot on its own stream, so a second batch's workgroups take the CUs the first batch's last
+// waves leave idle (its launch tail), and khb_collect retires the slots in submission order.
+struct Slot {
+  hipStream_t stream = nullptr;
+  Fe* d_scratch = nullptr;             // lane-private prefix scratch (allocated on the slot's first use)
+  AffPt* d_centres = nullptr;
+  AffPt* h_centres = nullptr;          // pinned staging
+  uint32_t centres_cap = 0;
+  khb_cand* d_cand = nullptr;
+  khb_degenerate* d_degen = nullptr;
+  uint32_t* d_ahits = nullptr;         // -m address hits
+  uint32_t* d_counters = nullptr;
+  uint32_t* h_counters = nullptr;      // pinned
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  uint64_t pending_steps = 0;
+  int kind = 0;                        // in flight: 1 = -m bsgs scan, 2 = -m address scan
+};
+constexpr int kQueueDepth = 2;
+
 struct khb_ctx {
   int device = -1;
-  hipStream_t stream = nullptr;
   int last_hip = 0;
   uint32_t lanes = 0;
   uint8_t* d_bloom = nullptr;
@@ -1128,22 +1147,12 @@ struct khb_ctx {
   uint32_t n_offs = 0, gpl = 0;
   AffPt* d_gofs = nullptr;             // per-group offsets expanded from gpl > 1 lane offsets
   bool gofs_stale = true;
-  AffPt* d_centres = nullptr;
-  uint32_t centres_cap = 0;
-  Fe* d_scratch = nullptr;
-  khb_cand* d_cand = nullptr;
-  khb_degenerate* d_degen = nullptr;
-  uint32_t* d_counters = nullptr;
-  uint32_t* h_counters = nullptr;      // pinned
-  AffPt* h_centres = nullptr;          // pinned staging
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool in_flight = false;
-  bool addr_in_flight = false;
-  uint64_t pending_steps = 0;
+  Slot slot[kQueueDepth];              // slot[0] also serves the synchronous helpers (dump, self-tests)
+  int head = 0;                        // oldest in-flight slot
+  int queued = 0;                      // submissions in flight (0..kQueueDepth)
   // -m address
   uint8_t* d_abloom = nullptr;
   BloomGeom ageom{};
-  uint32_t* d_ahits = nullptr;
 };
 
 namespace {
@@ -1161,32 +1170,72 @@ void pts_from_be(AffPt* dst, const uint8_t* src, uint32_t n) {
   }
 }
 
-// Groups the last launch walked (count_walked, copied back with the counters).
-uint64_t walked_groups(const khb_ctx* c) {
+// Groups the slot's last launch walked (count_walked, copied back with the counters).
+uint64_t walked_groups(const Slot& S) {
   uint64_t v;
-  memcpy(&v, c->h_counters + 4, sizeof v);
+  memcpy(&v, S.h_counters + 4, sizeof v);
   return v;
-}
-
-int ensure_centres(khb_ctx* c, uint32_t n) {
-  if (n <= c->centres_cap) return KHB_OK;
-  if (c->d_centres) hipFree(c->d_centres);
-  if (c->h_centres) hipHostFree(c->h_centres);
-  c->d_centres = nullptr;
-  c->h_centres = nullptr;
-  c->centres_cap = 0;
-  uint32_t cap = n < 1024 ? 1024 : n;
-  KHB_TRY(c, hipMalloc(&c->d_centres, sizeof(AffPt) * cap));
-  KHB_TRY(c, hipHostMalloc((void**)&c->h_centres, sizeof(AffPt) * cap, hipHostMallocDefault));
-  c->centres_cap = cap;
-  return KHB_OK;
 }
 
 // Entries (32 B) of lane-private scratch: scan_group needs 512, scan_batch kBatch*514 + kBatch.
 constexpr size_t kScratchEntries = (size_t)kBatch * (kHalf + 3) > kHalf ? (size_t)kBatch * (kHalf + 3) : kHalf;
 
+// Device state of a slot, created on its first use (a context that never queues a second
+// submission never pays for a second scratch).
+int ensure_slot(khb_ctx* c, Slot& S) {
+  if (S.d_scratch) return KHB_OK;
+  KHB_TRY(c, hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
+  KHB_TRY(c, hipMalloc(&S.d_scratch, sizeof(Fe) * kScratchEntries * c->lanes));
+  KHB_TRY(c, hipMalloc(&S.d_cand, sizeof(khb_cand) * kCandCap));
+  KHB_TRY(c, hipMalloc(&S.d_degen, sizeof(khb_degenerate) * kDegenCap));
+  KHB_TRY(c, hipMalloc(&S.d_counters, kCounterBytes));
+  KHB_TRY(c, hipHostMalloc((void**)&S.h_counters, kCounterBytes, hipHostMallocDefault));
+  KHB_TRY(c, hipEventCreate(&S.ev0));
+  KHB_TRY(c, hipEventCreate(&S.ev1));
+  return KHB_OK;
+}
+
+void free_slot(Slot& S) {
+  if (S.stream) hipStreamSynchronize(S.stream);
+  hipFree(S.d_scratch);
+  hipFree(S.d_centres);
+  hipFree(S.d_cand);
+  hipFree(S.d_degen);
+  hipFree(S.d_ahits);
+  hipFree(S.d_counters);
+  if (S.h_counters) hipHostFree(S.h_counters);
+  if (S.h_centres) hipHostFree(S.h_centres);
+  if (S.ev0) hipEventDestroy(S.ev0);
+  if (S.ev1) hipEventDestroy(S.ev1);
+  if (S.stream) hipStreamDestroy(S.stream);
+  S = Slot{};
+}
+
+int ensure_centres(khb_ctx* c, Slot& S, uint32_t n) {
+  if (n <= S.centres_cap) return KHB_OK;
+  if (S.d_centres) hipFree(S.d_centres);
+  if (S.h_centres) hipHostFree(S.h_centres);
+  S.d_centres = nullptr;
+  S.h_centres = nullptr;
+  S.centres_cap = 0;
+  uint32_t cap = n < 1024 ? 1024 : n;
+  KHB_TRY(c, hipMalloc(&S.d_centres, sizeof(AffPt) * cap));
+  KHB_TRY(c, hipHostMalloc((void**)&S.h_centres, sizeof(AffPt) * cap, hipHostMallocDefault));
+  S.centres_cap = cap;
+  return KHB_OK;
+}
+
+// The slot the next submission uses (KHB_EBUSY when every slot is in flight).
+Slot* next_slot(khb_ctx* c, int& rc) {
+  if (c->queued >= kQueueDepth) { rc = KHB_EBUSY; return nullptr; }
+  Slot& S = c->slot[(c->head + c->queued) % kQueueDepth];
+  rc = ensure_slot(c, S);
+  return rc ? nullptr : &S;
+}
+
 // per_item: groups per work item (the lane-offset stride gpl, or kBatch for scan_batch modes)
-ScanArgs make_args(khb_ctx* c, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count, uint32_t per_item = 0) {
+ScanArgs make_args(khb_ctx* c, const Slot& S, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count,
+                   uint32_t per_item = 0) {
   ScanArgs A{};
   if (per_item == 0) per_item = c->gpl;
   A.bloom = c->d_bloom;
@@ -1199,11 +1248,11 @@ ScanArgs make_args(khb_ctx* c, uint32_t n_jobs, uint32_t group_begin, uint32_t g
   A.gsn = c->d_gsn;
   A.offs = c->d_offs;
   A.gofs = c->gpl == 1 ? c->d_offs : c->d_gofs;
-  A.centres = c->d_centres;
-  A.scratch = c->d_scratch;
-  A.cand = c->d_cand;
-  A.degen = c->d_degen;
-  A.counters = c->d_counters;
+  A.centres = S.d_centres;
+  A.scratch = S.d_scratch;
+  A.cand = S.d_cand;
+  A.degen = S.d_degen;
+  A.counters = S.d_counters;
   A.n_jobs = n_jobs;
   A.group_begin = group_begin;
   A.group_end = group_begin + group_count;
@@ -1235,10 +1284,10 @@ int ensure_gofs(khb_ctx* c) {
   const uint32_t n = c->n_offs * c->gpl;
   if (c->d_gofs) { hipFree(c->d_gofs); c->d_gofs = nullptr; }
   KHB_TRY(c, hipMalloc(&c->d_gofs, sizeof(AffPt) * (size_t)n));
-  hipLaunchKernelGGL(k_expand_offsets, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->d_offs, c->gpl, c->d_gsn,
-                     c->d_gofs, n);
+  hipLaunchKernelGGL(k_expand_offsets, dim3((n + 255) / 256), dim3(256), 0, c->slot[0].stream, c->d_offs, c->gpl,
+                     c->d_gsn, c->d_gofs, n);
   KHB_TRY(c, hipGetLastError());
-  KHB_TRY(c, hipStreamSynchronize(c->stream));
+  KHB_TRY(c, hipStreamSynchronize(c->slot[0].stream));
   c->gofs_stale = false;
   return KHB_OK;
 }
@@ -1262,7 +1311,7 @@ const char* khb_strerror(int code) {
 }
 
 int khb_last_hip_error(const khb_ctx* c) { return c ? c->last_hip : 0; }
-void* khb_stream(khb_ctx* c) { return c ? (void*)c->stream : nullptr; }
+void* khb_stream(khb_ctx* c) { return c ? (void*)c->slot[0].stream : nullptr; }
 uint32_t khb_lanes(const khb_ctx* c) { return c ? c->lanes : 0; }
 uint32_t khb_groups_per_item(void) { return kBatch; }
 
@@ -1297,18 +1346,12 @@ int khb_open(int device, uint32_t lanes, khb_ctx** out) {
   if (lanes == 0) lanes = (uint32_t)prop.multiProcessorCount * 4u * KHB_WAVES_PER_SIMD * 64u;   // one full residency
   lanes = (lanes + kBlock - 1) / kBlock * kBlock;
   c->lanes = lanes;
-  int rc = KHB_OK;
-  auto fail = [&](hipError_t e) { rc = hip_fail(c, e); khb_close(c); return rc; };
-  hipError_t e;
-  if ((e = hipSetDevice(device)) != hipSuccess) return fail(e);
-  if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e);
-  if ((e = hipMalloc(&c->d_scratch, sizeof(Fe) * kScratchEntries * lanes)) != hipSuccess) return fail(e);
-  if ((e = hipMalloc(&c->d_cand, sizeof(khb_cand) * kCandCap)) != hipSuccess) return fail(e);
-  if ((e = hipMalloc(&c->d_degen, sizeof(khb_degenerate) * kDegenCap)) != hipSuccess) return fail(e);
-  if ((e = hipMalloc(&c->d_counters, kCounterBytes)) != hipSuccess) return fail(e);
-  if ((e = hipHostMalloc((void**)&c->h_counters, kCounterBytes, hipHostMallocDefault)) != hipSuccess) return fail(e);
-  if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return fail(e);
-  if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return fail(e);
+  hipError_t e = hipSetDevice(device);
+  int rc = e == hipSuccess ? ensure_slot(c, c->slot[0]) : hip_fail(c, e);
+  if (rc) {
+    khb_close(c);
+    return rc;
+  }
   *out = c;
   return KHB_OK;
 }
@@ -1316,25 +1359,14 @@ int khb_open(int device, uint32_t lanes, khb_ctx** out) {
 int khb_close(khb_ctx* c) {
   if (!c) return KHB_OK;
   if (c->device >= 0) hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
+  for (Slot& S : c->slot) free_slot(S);
   hipFree(c->d_bloom);
   hipFree(c->d_gate);
   hipFree(c->d_gate1);
   hipFree(c->d_gsn);
   hipFree(c->d_offs);
   hipFree(c->d_gofs);
-  hipFree(c->d_centres);
-  hipFree(c->d_scratch);
-  hipFree(c->d_cand);
-  hipFree(c->d_degen);
-  hipFree(c->d_counters);
   hipFree(c->d_abloom);
-  hipFree(c->d_ahits);
-  if (c->h_counters) hipHostFree(c->h_counters);
-  if (c->h_centres) hipHostFree(c->h_centres);
-  if (c->ev0) hipEventDestroy(c->ev0);
-  if (c->ev1) hipEventDestroy(c->ev1);
-  if (c->stream) hipStreamDestroy(c->stream);
   delete c;
   return KHB_OK;
 }
@@ -1342,7 +1374,7 @@ int khb_close(khb_ctx* c) {
 int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t probes) {
   if (!c || (gate && (log2_bits < 13 || log2_bits > 32 || probes < 1 || probes > KHB_GATE_MAX_PROBES)))
     return KHB_EINVAL;
-  if (c->in_flight) return KHB_EBUSY;
+  if (c->queued) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
   if (c->d_gate) { hipFree(c->d_gate); c->d_gate = nullptr; }
   if (c->d_gate1) { hipFree(c->d_gate1); c->d_gate1 = nullptr; }
@@ -1368,7 +1400,7 @@ int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t 
 
 int khb_set_gate_stage1(khb_ctx* c, uint32_t log2_bytes) {
   if (!c || (log2_bytes && (log2_bytes < 10 || log2_bytes > 31))) return KHB_EINVAL;
-  if (c->in_flight) return KHB_EBUSY;
+  if (c->queued) return KHB_EBUSY;
   c->gate1_log2 = log2_bytes;
   return KHB_OK;
 }
@@ -1376,7 +1408,7 @@ int khb_set_gate_stage1(khb_ctx* c, uint32_t log2_bytes) {
 int khb_load_bloom(khb_ctx* c, const uint8_t* bf, uint64_t bytes_per_sub, uint64_t bits_per_sub, uint32_t hashes) {
   if (!c || !bf || bytes_per_sub == 0 || bits_per_sub < 2 || hashes == 0 || hashes > 255) return KHB_EINVAL;
   if ((bits_per_sub + 7) / 8 != bytes_per_sub) return KHB_EINVAL;    // bloom.cpp:110-113
-  if (c->in_flight) return KHB_EBUSY;
+  if (c->queued) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
   if (c->d_bloom) { hipFree(c->d_bloom); c->d_bloom = nullptr; }
   const size_t total = (size_t)bytes_per_sub * 256;
@@ -1392,7 +1424,7 @@ int khb_load_bloom(khb_ctx* c, const uint8_t* bf, uint64_t bytes_per_sub, uint64
 
 int khb_load_giant_table(khb_ctx* c, const uint8_t* gsn) {
   if (!c || !gsn) return KHB_EINVAL;
-  if (c->in_flight) return KHB_EBUSY;
+  if (c->queued) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
   // 513 points, then p - x of each (the walk's negated table, GsnTable::nx)
   struct {
@@ -1410,7 +1442,7 @@ int khb_load_giant_table(khb_ctx* c, const uint8_t* gsn) {
 
 int khb_load_lane_offsets(khb_ctx* c, const uint8_t* offs, uint32_t n, uint32_t gpl) {
   if (!c || !offs || n == 0 || gpl == 0) return KHB_EINVAL;
-  if (c->in_flight) return KHB_EBUSY;
+  if (c->queued) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
   AffPt* h = (AffPt*)malloc(sizeof(AffPt) * n);
   if (!h) return KHB_ENOMEM;
@@ -1430,53 +1462,60 @@ int khb_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t gro
   int rc = check_scan_args(c, centres, n_jobs, group_begin, group_count);
   if (rc) return rc;
   if (!c->d_bloom) return KHB_ESTATE;
-  if (c->in_flight || c->addr_in_flight) return KHB_EBUSY;
+  if (c->queued && c->slot[c->head].kind != 1) return KHB_EBUSY;     // an -m address scan is in flight
   KHB_TRY(c, hipSetDevice(c->device));
-  if ((rc = ensure_centres(c, n_jobs)) || (rc = ensure_gofs(c))) return rc;
-  pts_from_be(c->h_centres, centres, n_jobs);
-  KHB_TRY(c, hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, c->stream));
-  KHB_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounterBytes, c->stream));
-  ScanArgs A = make_args(c, n_jobs, group_begin, group_count, kBatch);
+  Slot* Sp = next_slot(c, rc);
+  if (!Sp) return rc;
+  Slot& S = *Sp;
+  if ((rc = ensure_centres(c, S, n_jobs)) || (rc = ensure_gofs(c))) return rc;
+  ScanArgs A = make_args(c, S, n_jobs, group_begin, group_count, kBatch);
   if (A.n_items > 0xFFFFFF00ull) return KHB_EINVAL;      // the 32-bit work-item counter (KHB_DYN)
+  pts_from_be(S.h_centres, centres, n_jobs);
+  KHB_TRY(c, hipMemcpyAsync(S.d_centres, S.h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, S.stream));
+  KHB_TRY(c, hipMemsetAsync(S.d_counters, 0, kCounterBytes, S.stream));
   const uint32_t blocks = c->lanes / kBlock;
-  KHB_TRY(c, hipEventRecord(c->ev0, c->stream));
+  KHB_TRY(c, hipEventRecord(S.ev0, S.stream));
   if (c->d_gate1)
-    hipLaunchKernelGGL(k_giant_scan<kScanG1>, dim3(blocks), dim3(kBlock), 0, c->stream, A);
+    hipLaunchKernelGGL(k_giant_scan<kScanG1>, dim3(blocks), dim3(kBlock), 0, S.stream, A);
   else if (c->d_gate)
-    hipLaunchKernelGGL(k_giant_scan<kScanG>, dim3(blocks), dim3(kBlock), 0, c->stream, A);
+    hipLaunchKernelGGL(k_giant_scan<kScanG>, dim3(blocks), dim3(kBlock), 0, S.stream, A);
   else
-    hipLaunchKernelGGL(k_giant_scan<kScan>, dim3(blocks), dim3(kBlock), 0, c->stream, A);
+    hipLaunchKernelGGL(k_giant_scan<kScan>, dim3(blocks), dim3(kBlock), 0, S.stream, A);
   KHB_TRY(c, hipGetLastError());
-  KHB_TRY(c, hipEventRecord(c->ev1, c->stream));
-  KHB_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, kCounterBytes, hipMemcpyDeviceToHost, c->stream));
-  c->in_flight = true;
-  c->pending_steps = (uint64_t)n_jobs * group_count * KHB_GROUP;
+  KHB_TRY(c, hipEventRecord(S.ev1, S.stream));
+  KHB_TRY(c, hipMemcpyAsync(S.h_counters, S.d_counters, kCounterBytes, hipMemcpyDeviceToHost, S.stream));
+  S.kind = 1;
+  S.pending_steps = (uint64_t)n_jobs * group_count * KHB_GROUP;
+  c->queued++;
   return KHB_OK;
 }
 
 int khb_collect(khb_ctx* c, khb_cand* cand, uint32_t cap, khb_degenerate* degen, uint32_t degen_cap, khb_stats* st) {
   if (!c) return KHB_EINVAL;
-  if (!c->in_flight) return KHB_ESTATE;
+  if (!c->queued || c->slot[c->head].kind != 1) return KHB_ESTATE;
   KHB_TRY(c, hipSetDevice(c->device));
-  c->in_flight = false;
-  KHB_TRY(c, hipStreamSynchronize(c->stream));
-  const uint32_t nc = c->h_counters[0], nd = c->h_counters[1];
+  Slot& S = c->slot[c->head];
+  S.kind = 0;
+  c->head = (c->head + 1) % kQueueDepth;
+  c->queued--;
+  KHB_TRY(c, hipStreamSynchronize(S.stream));
+  const uint32_t nc = S.h_counters[0], nd = S.h_counters[1];
   uint32_t take = nc < kCandCap ? nc : kCandCap;
   if (take > cap) take = cap;
-  if (take && cand) KHB_TRY(c, hipMemcpy(cand, c->d_cand, sizeof(khb_cand) * take, hipMemcpyDeviceToHost));
+  if (take && cand) KHB_TRY(c, hipMemcpy(cand, S.d_cand, sizeof(khb_cand) * take, hipMemcpyDeviceToHost));
   uint32_t dt = nd < kDegenCap ? nd : kDegenCap;
   if (dt > degen_cap) dt = degen_cap;
-  if (dt && degen) KHB_TRY(c, hipMemcpy(degen, c->d_degen, sizeof(khb_degenerate) * dt, hipMemcpyDeviceToHost));
-  const uint64_t steps = walked_groups(c) * KHB_GROUP;
+  if (dt && degen) KHB_TRY(c, hipMemcpy(degen, S.d_degen, sizeof(khb_degenerate) * dt, hipMemcpyDeviceToHost));
+  const uint64_t steps = walked_groups(S) * KHB_GROUP;
   if (st) {
     st->n_cand = nc;
     st->n_degenerate = nd;
     st->giant_steps = steps;
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) ms = -1.f;
+    if (hipEventElapsedTime(&ms, S.ev0, S.ev1) != hipSuccess) ms = -1.f;
     st->kernel_ms = ms;
   }
-  return steps == c->pending_steps ? KHB_OK : KHB_EINCOMPLETE;
+  return steps == S.pending_steps ? KHB_OK : KHB_EINCOMPLETE;
 }
 
 int khb_scan(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count,
@@ -1490,24 +1529,25 @@ int khb_dump_x(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint32_t
   int rc = check_scan_args(c, centre, 1, group_begin, group_count);
   if (rc) return rc;
   if (!xs) return KHB_EINVAL;
-  if (c->in_flight) return KHB_EBUSY;
+  if (c->queued) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
-  if ((rc = ensure_centres(c, 1)) || (rc = ensure_gofs(c))) return rc;
-  pts_from_be(c->h_centres, centre, 1);
+  Slot& S = c->slot[0];
+  if ((rc = ensure_centres(c, S, 1)) || (rc = ensure_gofs(c))) return rc;
+  pts_from_be(S.h_centres, centre, 1);
   const size_t bytes = (size_t)group_count * KHB_GROUP * 32;
   uint8_t* d_x = nullptr;
   KHB_TRY(c, hipMalloc(&d_x, bytes));
-  hipError_t e = hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt), hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, kCounterBytes, c->stream);
+  hipError_t e = hipMemcpyAsync(S.d_centres, S.h_centres, sizeof(AffPt), hipMemcpyHostToDevice, S.stream);
+  if (e == hipSuccess) e = hipMemsetAsync(S.d_counters, 0, kCounterBytes, S.stream);
   if (e == hipSuccess) {
-    ScanArgs A = make_args(c, 1, group_begin, group_count, kBatch);
+    ScanArgs A = make_args(c, S, 1, group_begin, group_count, kBatch);
     A.xdump = d_x;
     const uint32_t blocks = (uint32_t)((A.n_items + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_giant_scan<kDump>, dim3(blocks < c->lanes / kBlock ? blocks : c->lanes / kBlock),
-                       dim3(kBlock), 0, c->stream, A);
+                       dim3(kBlock), 0, S.stream, A);
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(S.stream);
   if (e == hipSuccess) e = hipMemcpy(xs, d_x, bytes, hipMemcpyDeviceToHost);
   hipFree(d_x);
   if (e != hipSuccess) return hip_fail(c, e);
@@ -1517,6 +1557,7 @@ int khb_dump_x(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint32_t
 int khb_field_op(khb_ctx* c, int op, const uint8_t* a, const uint8_t* b, uint8_t* r, uint32_t n) {
   if (!c || !a || !r || n == 0 || op < 0 || op > 6 || (op != 1 && op != 4 && !b)) return KHB_EINVAL;
   KHB_TRY(c, hipSetDevice(c->device));
+  Slot& S = c->slot[0];
   Fe* h = (Fe*)malloc(sizeof(Fe) * n * 3);
   if (!h) return KHB_ENOMEM;
   for (uint32_t i = 0; i < n; ++i) {
@@ -1527,10 +1568,10 @@ int khb_field_op(khb_ctx* c, int op, const uint8_t* a, const uint8_t* b, uint8_t
   hipError_t e = hipMalloc(&d, sizeof(Fe) * n * 3);
   if (e == hipSuccess) e = hipMemcpy(d, h, sizeof(Fe) * n * 2, hipMemcpyHostToDevice);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(k_field_op, dim3((n + 255) / 256), dim3(256), 0, c->stream, op, d, d + n, d + 2 * n, n);
+    hipLaunchKernelGGL(k_field_op, dim3((n + 255) / 256), dim3(256), 0, S.stream, op, d, d + n, d + 2 * n, n);
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(S.stream);
   if (e == hipSuccess) e = hipMemcpy(h + 2 * n, d + 2 * n, sizeof(Fe) * n, hipMemcpyDeviceToHost);
   if (e == hipSuccess)
     for (uint32_t i = 0; i < n; ++i) fe_to_be(r + 32 * (size_t)i, h[2 * n + i]);
@@ -1544,6 +1585,7 @@ int khb_probe(khb_ctx* c, const uint8_t* xs, uint8_t* hit, uint32_t n) {
   if (!c || !xs || !hit || n == 0) return KHB_EINVAL;
   if (!c->d_bloom) return KHB_ESTATE;
   KHB_TRY(c, hipSetDevice(c->device));
+  Slot& S = c->slot[0];
   Fe* h = (Fe*)malloc(sizeof(Fe) * n);
   if (!h) return KHB_ENOMEM;
   for (uint32_t i = 0; i < n; ++i) fe_from_be(h[i], xs + 32 * (size_t)i);
@@ -1553,10 +1595,10 @@ int khb_probe(khb_ctx* c, const uint8_t* xs, uint8_t* hit, uint32_t n) {
   if (e == hipSuccess) e = hipMalloc(&dh, n);
   if (e == hipSuccess) e = hipMemcpy(d, h, sizeof(Fe) * n, hipMemcpyHostToDevice);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(k_probe, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->d_bloom, c->geom, d, dh, n);
+    hipLaunchKernelGGL(k_probe, dim3((n + 255) / 256), dim3(256), 0, S.stream, c->d_bloom, c->geom, d, dh, n);
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(S.stream);
   if (e == hipSuccess) e = hipMemcpy(hit, dh, n, hipMemcpyDeviceToHost);
   hipFree(d);
   hipFree(dh);
@@ -1570,7 +1612,7 @@ int khb_probe(khb_ctx* c, const uint8_t* xs, uint8_t* hit, uint32_t n) {
 int khb_load_addr_bloom(khb_ctx* c, const uint8_t* bf, uint64_t bytes, uint64_t bits, uint32_t hashes) {
   if (!c || !bf || bytes == 0 || bits < 2 || hashes == 0 || hashes > 255) return KHB_EINVAL;
   if ((bits + 7) / 8 != bytes) return KHB_EINVAL;    // bloom.cpp:110-113
-  if (c->in_flight || c->addr_in_flight) return KHB_EBUSY;
+  if (c->queued) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
   if (c->d_abloom) { hipFree(c->d_abloom); c->d_abloom = nullptr; }
   KHB_TRY(c, hipMalloc(&c->d_abloom, bytes));
@@ -1580,7 +1622,6 @@ int khb_load_addr_bloom(khb_ctx* c, const uint8_t* bf, uint64_t bytes, uint64_t 
   c->ageom.magic = (uint64_t)(((unsigned __int128)1 << 64) / bits);
   c->ageom.wrap = (uint64_t)(((unsigned __int128)1 << 64) % bits);
   c->ageom.hashes = hashes;
-  if (!c->d_ahits) KHB_TRY(c, hipMalloc(&c->d_ahits, sizeof(khb_addr_hit) * kAddrHitCap));
   return KHB_OK;
 }
 
@@ -1590,52 +1631,60 @@ int khb_addr_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_
   if (rc) return rc;
   if (search < 0 || search > 2) return KHB_EINVAL;
   if (!c->d_abloom) return KHB_ESTATE;
-  if (c->in_flight || c->addr_in_flight) return KHB_EBUSY;
+  if (c->queued && c->slot[c->head].kind != 2) return KHB_EBUSY;     // an -m bsgs scan is in flight
   KHB_TRY(c, hipSetDevice(c->device));
-  if ((rc = ensure_centres(c, n_jobs))) return rc;
-  pts_from_be(c->h_centres, centres, n_jobs);
-  KHB_TRY(c, hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, c->stream));
-  KHB_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounterBytes, c->stream));
-  ScanArgs A = make_args(c, n_jobs, group_begin, group_count);
+  Slot* Sp = next_slot(c, rc);
+  if (!Sp) return rc;
+  Slot& S = *Sp;
+  if ((rc = ensure_centres(c, S, n_jobs))) return rc;
+  if (!S.d_ahits) KHB_TRY(c, hipMalloc(&S.d_ahits, sizeof(khb_addr_hit) * kAddrHitCap));
+  pts_from_be(S.h_centres, centres, n_jobs);
+  KHB_TRY(c, hipMemcpyAsync(S.d_centres, S.h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, S.stream));
+  KHB_TRY(c, hipMemsetAsync(S.d_counters, 0, kCounterBytes, S.stream));
+  ScanArgs A = make_args(c, S, n_jobs, group_begin, group_count);
   A.bloom = c->d_abloom;
   A.geom = c->ageom;
-  A.ahits = c->d_ahits;
+  A.ahits = S.d_ahits;
   A.ahit_cap = kAddrHitCap;
   const uint32_t blocks = c->lanes / kBlock;
-  KHB_TRY(c, hipEventRecord(c->ev0, c->stream));
+  KHB_TRY(c, hipEventRecord(S.ev0, S.stream));
   switch (search) {
-    case 0: hipLaunchKernelGGL(k_giant_scan<kAddrU>, dim3(blocks), dim3(kBlock), 0, c->stream, A); break;
-    case 1: hipLaunchKernelGGL(k_giant_scan<kAddrC>, dim3(blocks), dim3(kBlock), 0, c->stream, A); break;
-    default: hipLaunchKernelGGL(k_giant_scan<kAddrB>, dim3(blocks), dim3(kBlock), 0, c->stream, A); break;
+    case 0: hipLaunchKernelGGL(k_giant_scan<kAddrU>, dim3(blocks), dim3(kBlock), 0, S.stream, A); break;
+    case 1: hipLaunchKernelGGL(k_giant_scan<kAddrC>, dim3(blocks), dim3(kBlock), 0, S.stream, A); break;
+    default: hipLaunchKernelGGL(k_giant_scan<kAddrB>, dim3(blocks), dim3(kBlock), 0, S.stream, A); break;
   }
   KHB_TRY(c, hipGetLastError());
-  KHB_TRY(c, hipEventRecord(c->ev1, c->stream));
-  KHB_TRY(c, hipMemcpyAsync(c->h_counters, c->d_counters, kCounterBytes, hipMemcpyDeviceToHost, c->stream));
-  c->addr_in_flight = true;
-  c->pending_steps = (uint64_t)n_jobs * group_count * KHB_GROUP;
+  KHB_TRY(c, hipEventRecord(S.ev1, S.stream));
+  KHB_TRY(c, hipMemcpyAsync(S.h_counters, S.d_counters, kCounterBytes, hipMemcpyDeviceToHost, S.stream));
+  S.kind = 2;
+  S.pending_steps = (uint64_t)n_jobs * group_count * KHB_GROUP;
+  c->queued++;
   return KHB_OK;
 }
 
 int khb_addr_collect(khb_ctx* c, khb_addr_hit* hits, uint32_t cap, khb_stats* st) {
   if (!c) return KHB_EINVAL;
-  if (!c->addr_in_flight) return KHB_ESTATE;
+  if (!c->queued || c->slot[c->head].kind != 2) return KHB_ESTATE;
   KHB_TRY(c, hipSetDevice(c->device));
-  c->addr_in_flight = false;
-  KHB_TRY(c, hipStreamSynchronize(c->stream));
-  const uint32_t nh = c->h_counters[0], nd = c->h_counters[1];
+  Slot& S = c->slot[c->head];
+  S.kind = 0;
+  c->head = (c->head + 1) % kQueueDepth;
+  c->queued--;
+  KHB_TRY(c, hipStreamSynchronize(S.stream));
+  const uint32_t nh = S.h_counters[0], nd = S.h_counters[1];
   uint32_t take = nh < kAddrHitCap ? nh : kAddrHitCap;
   if (take > cap) take = cap;
-  if (take && hits) KHB_TRY(c, hipMemcpy(hits, c->d_ahits, sizeof(khb_addr_hit) * take, hipMemcpyDeviceToHost));
-  const uint64_t steps = walked_groups(c) * KHB_GROUP;
+  if (take && hits) KHB_TRY(c, hipMemcpy(hits, S.d_ahits, sizeof(khb_addr_hit) * take, hipMemcpyDeviceToHost));
+  const uint64_t steps = walked_groups(S) * KHB_GROUP;
   if (st) {
     st->n_cand = nh;
     st->n_degenerate = nd;
     st->giant_steps = steps;
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) ms = -1.f;
+    if (hipEventElapsedTime(&ms, S.ev0, S.ev1) != hipSuccess) ms = -1.f;
     st->kernel_ms = ms;
   }
-  return steps == c->pending_steps ? KHB_OK : KHB_EINCOMPLETE;
+  return steps == S.pending_steps ? KHB_OK : KHB_EINCOMPLETE;
 }
 
 int khb_addr_scan(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count,
@@ -1649,24 +1698,25 @@ int khb_addr_dump(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint3
   int rc = check_scan_args(c, centre, 1, group_begin, group_count, false);
   if (rc) return rc;
   if (!xy) return KHB_EINVAL;
-  if (c->in_flight || c->addr_in_flight) return KHB_EBUSY;
+  if (c->queued) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
-  if ((rc = ensure_centres(c, 1))) return rc;
-  pts_from_be(c->h_centres, centre, 1);
+  Slot& S = c->slot[0];
+  if ((rc = ensure_centres(c, S, 1))) return rc;
+  pts_from_be(S.h_centres, centre, 1);
   const size_t bytes = (size_t)group_count * KHB_GROUP * 64;
   uint8_t* d_xy = nullptr;
   KHB_TRY(c, hipMalloc(&d_xy, bytes));
-  hipError_t e = hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt), hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, kCounterBytes, c->stream);
+  hipError_t e = hipMemcpyAsync(S.d_centres, S.h_centres, sizeof(AffPt), hipMemcpyHostToDevice, S.stream);
+  if (e == hipSuccess) e = hipMemsetAsync(S.d_counters, 0, kCounterBytes, S.stream);
   if (e == hipSuccess) {
-    ScanArgs A = make_args(c, 1, group_begin, group_count);
+    ScanArgs A = make_args(c, S, 1, group_begin, group_count);
     A.xdump = d_xy;
     const uint32_t blocks = (uint32_t)((A.n_items + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_giant_scan<kAddrDump>, dim3(blocks < c->lanes / kBlock ? blocks : c->lanes / kBlock),
-                       dim3(kBlock), 0, c->stream, A);
+                       dim3(kBlock), 0, S.stream, A);
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(S.stream);
   if (e == hipSuccess) e = hipMemcpy(xy, d_xy, bytes, hipMemcpyDeviceToHost);
   hipFree(d_xy);
   if (e != hipSuccess) return hip_fail(c, e);
@@ -1676,6 +1726,7 @@ int khb_addr_dump(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint3
 int khb_hash160(khb_ctx* c, int kind, const uint8_t* xy, uint8_t* out, uint32_t n) {
   if (!c || !xy || !out || n == 0 || kind < 0 || kind > 2) return KHB_EINVAL;
   KHB_TRY(c, hipSetDevice(c->device));
+  Slot& S = c->slot[0];
   AffPt* h = (AffPt*)malloc(sizeof(AffPt) * n);
   if (!h) return KHB_ENOMEM;
   pts_from_be(h, xy, n);
@@ -1685,11 +1736,11 @@ int khb_hash160(khb_ctx* c, int kind, const uint8_t* xy, uint8_t* out, uint32_t 
   if (e == hipSuccess) e = hipMalloc(&dout, 21 * (size_t)n);
   if (e == hipSuccess) e = hipMemcpy(d, h, sizeof(AffPt) * n, hipMemcpyHostToDevice);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(k_hash160, dim3((n + 255) / 256), dim3(256), 0, c->stream, (const Fe*)d, kind, c->d_abloom,
+    hipLaunchKernelGGL(k_hash160, dim3((n + 255) / 256), dim3(256), 0, S.stream, (const Fe*)d, kind, c->d_abloom,
                        c->ageom, dout, n);
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(S.stream);
   if (e == hipSuccess) e = hipMemcpy(out, dout, 21 * (size_t)n, hipMemcpyDeviceToHost);
   hipFree(d);
   hipFree(dout);
@@ -1714,11 +1765,12 @@ int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t
     if (outs[l] && (bits_per_sub[l] < 2 || (bits_per_sub[l] + 7) / 8 != bytes_per_sub[l] || hashes[l] == 0 ||
                     hashes[l] > 255))
       return KHB_EINVAL;
-  if (c->in_flight || c->addr_in_flight) return KHB_EBUSY;
+  if (c->queued) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
-  if ((rc = ensure_centres(c, n_jobs))) return rc;
-  pts_from_be(c->h_centres, centres, n_jobs);
-  ScanArgs A = make_args(c, n_jobs, 0, groups_per_job);
+  Slot& S = c->slot[0];
+  if ((rc = ensure_centres(c, S, n_jobs))) return rc;
+  pts_from_be(S.h_centres, centres, n_jobs);
+  ScanArgs A = make_args(c, S, n_jobs, 0, groups_per_job);
   A.job_keys = (uint64_t)groups_per_job * KHB_GROUP;
   A.blimit[0] = l1 ? l1ext : 0;
   A.blimit[1] = l2 ? m2 : 0;
@@ -1730,7 +1782,7 @@ int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t
   hipError_t e = hipSuccess;
   if (gate) {
     e = hipMalloc(&dgate, gate_bytes);
-    if (e == hipSuccess) e = hipMemsetAsync(dgate, 0, gate_bytes, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(dgate, 0, gate_bytes, S.stream);
     A.gate_w = dgate;
     A.glimit = l1ext;
     A.gate_mask = (uint32_t)((1ull << (gate_log2 - 6)) - 1);
@@ -1740,7 +1792,7 @@ int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t
     if (!outs[l]) continue;
     const uint64_t words = (bytes_per_sub[l] + 3) / 4;
     e = hipMalloc(&dw[l], 256 * words * 4);
-    if (e == hipSuccess) e = hipMemsetAsync(dw[l], 0, 256 * words * 4, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(dw[l], 0, 256 * words * 4, S.stream);
     A.bw[l] = dw[l];
     A.bwords[l] = words;
     BloomGeom& g = A.bgeom[l];
@@ -1755,21 +1807,21 @@ int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t
     A.bp = dbp;
   }
   if (e == hipSuccess)
-    e = hipMemcpyAsync(c->d_centres, c->h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, kCounterBytes, c->stream);
-  if (e == hipSuccess) e = hipEventRecord(c->ev0, c->stream);
+    e = hipMemcpyAsync(S.d_centres, S.h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, S.stream);
+  if (e == hipSuccess) e = hipMemsetAsync(S.d_counters, 0, kCounterBytes, S.stream);
+  if (e == hipSuccess) e = hipEventRecord(S.ev0, S.stream);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(k_giant_scan<kBaby>, dim3(c->lanes / kBlock), dim3(kBlock), 0, c->stream, A);
+    hipLaunchKernelGGL(k_giant_scan<kBaby>, dim3(c->lanes / kBlock), dim3(kBlock), 0, S.stream, A);
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipEventRecord(c->ev1, c->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipEventRecord(S.ev1, S.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(S.stream);
   uint64_t walked = 0;
-  if (e == hipSuccess) e = hipMemcpy(c->h_counters, c->d_counters, kCounterBytes, hipMemcpyDeviceToHost);
-  if (e == hipSuccess) walked = walked_groups(c);
+  if (e == hipSuccess) e = hipMemcpy(S.h_counters, S.d_counters, kCounterBytes, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) walked = walked_groups(S);
   if (e == hipSuccess && kernel_ms) {
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) ms = -1.f;
+    if (hipEventElapsedTime(&ms, S.ev0, S.ev1) != hipSuccess) ms = -1.f;
     *kernel_ms = ms;
   }
   for (int l = 0; l < 3 && e == hipSuccess; ++l) {

@@ -82,3 +82,38 @@ def test_device_step_count_matches_submission():
             _, _, st = e.scan(centres, g0, gc)
             assert st.giant_steps == n_jobs * gc * 1024
     t.close()
+
+
+def test_two_queued_submissions_fifo(ora):
+    """khb_submit twice before collecting (the context's two slots, one stream each): each collect
+    returns its own submission's candidates in submission order, a third submission is refused with
+    KHB_EBUSY while both are in flight, and the candidates equal the oracle's."""
+    from keyhuntm1cpu_amd.khbsgs import Engine, KhbError
+    t = khhost.Tables("0x100000000", 1, threads=8)
+    o = ora.Bsgs("0x100000000", 1, 8)
+    key = 0x2000000000123457
+    tgt = ora.pubkey(key)
+    batches = [[0x2000000000000000 + (3 * b + c) * (1 << 33) for c in range(3)] for b in range(3)]
+    with Engine(0, lanes=16384) as e:
+        bf, nb, bits, h = t.bloom_concat(1)
+        e.load_bloom(bf, nb, bits, h)
+        e.load_giant_table(t.giant_table())
+        offs, gpl = t.lane_offsets()
+        e.load_lane_offsets(offs, gpl)
+        cent = [b"".join(t.chunk_centre(b, tgt.be64()) for b in bs) for bs in batches]
+        e.submit(cent[0], 0, t.cycles)
+        e.submit(cent[1], 0, t.cycles)
+        with pytest.raises(KhbError, match="in flight"):
+            e.submit(cent[2], 0, t.cycles)
+        got = [e.collect()]
+        e.submit(cent[2], 0, t.cycles)
+        got += [e.collect(), e.collect()]
+        with pytest.raises(KhbError, match="call order"):
+            e.collect()
+    for bs, (cands, degen, st) in zip(batches, got):
+        assert st.giant_steps == 3 * t.cycles * 1024 and not degen
+        for j, b in enumerate(bs):
+            ref, _, _ = o.scan(o.chunk_start(b, tgt), 0, o.cycles)
+            assert sorted(a for jj, a in cands if jj == j) == sorted(ref)
+    assert [a for jj, a in got[0][0] if jj == 0]         # the key's chunk (batch 0, chunk 0) has a hit
+    t.close()
