@@ -14,7 +14,11 @@ BINDIR   := $(PKG)/bin
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wno-unused-result -Wno-unused-value
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -march=x86-64-v3 -Wall -Wextra -Wno-unused-function -Wno-unused-parameter -Wno-unknown-pragmas -pthread
 
-DEV_HDRS  := $(wildcard $(CSRC)/device/*.hpp) include/khbsgs.h
+DEV_HDRS  := $(wildcard $(CSRC)/device/*.hpp) $(CSRC)/scan_kernels.hpp include/khbsgs.h
+# libkhbsgs: the C ABI (khbsgs.hip) + one translation unit per group of k_giant_scan instances, so
+# `make -j` compiles the heavy kernels in parallel
+HIP_SRCS  := $(CSRC)/khbsgs.hip $(CSRC)/k_bsgs.hip $(CSRC)/k_addr.hip $(CSRC)/k_baby.hip
+HIP_OBJS  := $(patsubst $(CSRC)/%.hip,build/hip/%.o,$(HIP_SRCS))
 HOST_SRCS := $(CSRC)/host/u256.cpp $(CSRC)/host/secp_host.cpp $(CSRC)/host/bloom_host.cpp \
              $(CSRC)/host/bsgs_host.cpp $(CSRC)/host/bsgs_files.cpp $(CSRC)/host/engine.cpp \
              $(CSRC)/host/address_host.cpp
@@ -23,11 +27,14 @@ HOST_OBJS := $(patsubst $(CSRC)/host/%.cpp,build/host/%.o,$(HOST_SRCS))
 
 all: $(LIBDIR)/libkhbsgs.so $(LIBDIR)/libkhhost.so $(BINDIR)/keyhunt_amd $(BINDIR)/bsgsd_amd oracle
 
-$(LIBDIR) $(BINDIR) build/host:
+$(LIBDIR) $(BINDIR) build/host build/hip:
 	mkdir -p $@
 
-$(LIBDIR)/libkhbsgs.so: $(CSRC)/khbsgs.hip $(DEV_HDRS) | $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CSRC)/khbsgs.hip
+build/hip/%.o: $(CSRC)/%.hip $(DEV_HDRS) | build/hip
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIBDIR)/libkhbsgs.so: $(HIP_OBJS) | $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_OBJS)
 
 build/host/%.o: $(CSRC)/host/%.cpp $(HOST_HDRS) | build/host
 	$(CXX) $(CXXFLAGS) -c -o $@ $<
@@ -53,58 +60,58 @@ clean:
 # Kernel variants for A/B timing (tools/perf_variants.py); not used by the product.
 VARIANTS := r2
 variants: $(patsubst %,$(LIBDIR)/variants/libkhbsgs_%.so,$(VARIANTS))
-$(LIBDIR)/variants/libkhbsgs_w%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+$(LIBDIR)/variants/libkhbsgs_w%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_WAVES_PER_SIMD=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_r%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_WAVES_PER_SIMD=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_r%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_PROBE_BITS=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_g%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_PROBE_BITS=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_g%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_GSN_SCALAR=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_m0s%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_GSN_SCALAR=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_m0s%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_MUL_IMPL=0 -DKHB_SQR_IMPL=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_m1s%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_MUL_IMPL=0 -DKHB_SQR_IMPL=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_m1s%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_MUL_IMPL=1 -DKHB_SQR_IMPL=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_m2s%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_MUL_IMPL=1 -DKHB_SQR_IMPL=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_m2s%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_MUL_IMPL=2 -DKHB_SQR_IMPL=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_p%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_MUL_IMPL=2 -DKHB_SQR_IMPL=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_p%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_PROBE_MODE=$* -shared -o $@ $(CSRC)/khbsgs.hip
+	$(HIPCC) $(HIPFLAGS) -DKHB_PROBE_MODE=$* -shared -o $@ $(HIP_SRCS)
 .PHONY: variants
-$(LIBDIR)/variants/libkhbsgs_q%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+$(LIBDIR)/variants/libkhbsgs_q%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_PIPE=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_b%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_PIPE=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_b%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_BATCH=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_f%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_BATCH=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_f%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_FUSE=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_c%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_FUSE=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_c%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_LDSCOUNT=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_n%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_LDSCOUNT=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_n%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_NT=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_x%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_NT=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_x%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_RARE=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_xf.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_RARE=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_xf.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_RARE_FORCE=1 -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_nonop.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_RARE_FORCE=1 -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_nonop.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_NONOP=1 -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_h%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_NONOP=1 -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_h%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_GATE1=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_gnt%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_GATE1=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_gnt%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_GATE_NT=$* -shared -o $@ $(CSRC)/khbsgs.hip
-$(LIBDIR)/variants/libkhbsgs_dyn%.so: $(CSRC)/khbsgs.hip $(DEV_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DKHB_GATE_NT=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_dyn%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
-	$(HIPCC) $(HIPFLAGS) -DKHB_DYN=$* -shared -o $@ $(CSRC)/khbsgs.hip
+	$(HIPCC) $(HIPFLAGS) -DKHB_DYN=$* -shared -o $@ $(HIP_SRCS)

@@ -1,0 +1,16 @@
+// k_giant_scan instances for -m bsgs scan (ungated, gated, gated with the stage-1 fold) and the x dump (scan_kernels.hpp).
+#include "scan_kernels.hpp"
+
+namespace khbk {
+
+void launch_bsgs(int mode, uint32_t blocks, hipStream_t stream, const ScanArgs& A) {
+  switch (mode) {
+    case kScan: hipLaunchKernelGGL(k_giant_scan<kScan>, dim3(blocks), dim3(kBlock), 0, stream, A); break;
+    case kScanG: hipLaunchKernelGGL(k_giant_scan<kScanG>, dim3(blocks), dim3(kBlock), 0, stream, A); break;
+    case kScanG1: hipLaunchKernelGGL(k_giant_scan<kScanG1>, dim3(blocks), dim3(kBlock), 0, stream, A); break;
+    case kDump: hipLaunchKernelGGL(k_giant_scan<kDump>, dim3(blocks), dim3(kBlock), 0, stream, A); break;
+    default: break;
+  }
+}
+
+}  // namespace khbk
