@@ -25,7 +25,7 @@ HOST_SRCS := $(CSRC)/host/u256.cpp $(CSRC)/host/secp_host.cpp $(CSRC)/host/bloom
 HOST_HDRS := $(wildcard $(CSRC)/host/*.hpp) $(DEV_HDRS) include/khhost.h
 HOST_OBJS := $(patsubst $(CSRC)/host/%.cpp,build/host/%.o,$(HOST_SRCS))
 
-all: $(LIBDIR)/libkhbsgs.so $(LIBDIR)/libkhhost.so $(BINDIR)/keyhunt_amd $(BINDIR)/bsgsd_amd oracle
+all: $(LIBDIR)/libkhbsgs.so $(LIBDIR)/libkhbsgs_f9.so $(LIBDIR)/libkhhost.so $(BINDIR)/keyhunt_amd $(BINDIR)/bsgsd_amd oracle
 
 $(LIBDIR) $(BINDIR) build/host build/hip:
 	mkdir -p $@
@@ -35,6 +35,13 @@ build/hip/%.o: $(CSRC)/%.hip $(DEV_HDRS) | build/hip
 
 $(LIBDIR)/libkhbsgs.so: $(HIP_OBJS) | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_OBJS)
+
+# The same library with the gated scan in 9 x 29-bit limbs (KHB_F9WALK=1, device/fe29.hpp): an
+# alternative build kept parity-tested (tests/test_gpu_f9walk.py); the product uses the 8 x 32 walk.
+build/hip/%_f9.o: $(CSRC)/%.hip $(DEV_HDRS) | build/hip
+	$(HIPCC) $(HIPFLAGS) -DKHB_F9WALK=1 -c -o $@ $<
+$(LIBDIR)/libkhbsgs_f9.so: build/hip/khbsgs_f9.o build/hip/k_bsgs_f9.o build/hip/k_addr.o build/hip/k_baby.o | $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 build/host/%.o: $(CSRC)/host/%.cpp $(HOST_HDRS) | build/host
 	$(CXX) $(CXXFLAGS) -c -o $@ $<
@@ -115,3 +122,9 @@ $(LIBDIR)/variants/libkhbsgs_gnt%.so: $(HIP_SRCS) $(DEV_HDRS)
 $(LIBDIR)/variants/libkhbsgs_dyn%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) -DKHB_DYN=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_f9w%.so: $(HIP_SRCS) $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_F9WALK=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_cnv%.so: $(HIP_SRCS) $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_CN_VOLATILE=$* -shared -o $@ $(HIP_SRCS)

@@ -128,7 +128,7 @@ int khb_scan(khb_ctx* ctx, const uint8_t* centres_xy_be, uint32_t n_jobs, uint32
 
 /* ---- parity / debug ---- */
 /* x-coordinates (BE, probe order t = 0..1023 per group) of groups [group_begin,
- * group_begin+group_count) of ONE job; xs must hold group_count*1024*32 bytes. */
+ * group_begin+group_count) of ONE job; xs must hold group_count*1024*32 bytes, canonical. */
 int khb_dump_x(khb_ctx* ctx, const uint8_t* centre_xy_be, uint32_t group_begin, uint32_t group_count,
                uint8_t* xs);
 /* Field self-test kernel: r[i] = op(a[i], b[i]) mod p, canonical, for op 0=mul 1=sqr 2=add 3=sub

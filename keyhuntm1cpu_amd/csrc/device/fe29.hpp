@@ -11,8 +11,9 @@
 //   * an F9 holds x = sum v[i] 2^(29 i), congruent to the field element, not reduced;
 //   * "strict" limbs: v[i] < 2^29 + 2^20 (every f9_mul / f9_sqr result; f9_from_fe output < 2^29);
 //   * f9_mul / f9_sqr accept limbs < 2^30.4 on both operands (a column of nine products then stays
-//     below 9 * 2^60.8 < 2^64 and the folds below add < 2^56), so the sum of two strict values
-//     (f9_add) is a valid operand;
+//     below 9 * 2^60.8 < 2^64 and the folds below add < 2^51), so the sum of two strict values
+//     (f9_add) is a valid operand; more generally any operands whose limb bounds multiply to less
+//     than 2^60.8 (e.g. < 2^31.6 against a strict product result);
 //   * f9_gate_words returns the low 64 bits of the canonical value (x mod p) for limbs < 2^30.6,
 //     and flags the rare inputs (probability ~2^-22) for which that fast path is not exact;
 //   * f9_to_fe returns the canonical 8 x 32 form of any value with limbs < 2^31.
@@ -38,14 +39,42 @@ KHB_HD void f9_add(F9& r, const F9& a, const F9& b) {
   for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] + b.v[i];
 }
 
-// acc += a * b (one v_mad_u64_u32 on the device: the 64-bit addend is the accumulator itself, so no
-// zero-extension moves; the compiler would turn multiplications by 256 / 2048 into 64-bit shifts of
-// zero-extended operands).
-KHB_HD void f9_mad(uint64_t& acc, uint32_t a, uint32_t b) {
+// x = a + 2p - b, limb-wise with 2p written so that every limb is >= 2^29 (>= 2^24 for limb 8):
+// for strict b (limbs < 2^29, limb 8 < 2^24: canonical values from f9_from_fe) no limb borrows, and
+// the limbs of the result stay < a + 2^30.
+KHB_HD void f9_add_neg(F9& r, const F9& a, const F9& b) {
+  const uint32_t K[9] = {0x3ffff85eu, 0x3fffffeeu, 0x3ffffffeu, 0x3ffffffeu, 0x3ffffffeu,
+                         0x3ffffffeu, 0x3ffffffeu, 0x3ffffffeu, 0x1fffffeu};
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] + (K[i] - b.v[i]);
+}
+
+// A constant the compiler cannot see through (an SGPR written by s_mov_b32): products by it stay
+// one v_mad_u64_u32 each, where the known powers of two 256 / 2048 would become 64-bit shifts of
+// zero-extended operands (two moves and a shift more per fold).  Inline-asm multiplies would do the
+// same at the price of an s_nop after each (the compiler pads asm for the VCC / SGPR hazards).
+KHB_HD uint32_t f9_k(uint32_t k) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
+  uint32_t r;
+  asm("s_mov_b32 %0, %1" : "=s"(r) : "i"(k));
+  return r;
 #else
-  acc += (uint64_t)a * b;
+  return k;
+#endif
+}
+
+// acc += a * b
+KHB_HD void f9_mad(uint64_t& acc, uint32_t a, uint32_t b) { acc += (uint64_t)a * b; }
+
+// Scheduling fence (KHB_F9_FENCE): keeps the compiler from hoisting every partial product of a
+// multiply to its start, which would hold all 17 columns live at once (register pressure at 4
+// waves/SIMD); the products of one column still issue back to back.
+#ifndef KHB_F9_FENCE
+#define KHB_F9_FENCE 1
+#endif
+KHB_HD void f9_fence() {
+#if defined(__HIP_DEVICE_COMPILE__) && KHB_F9_FENCE
+  __builtin_amdgcn_sched_barrier(0);
 #endif
 }
 
@@ -63,23 +92,23 @@ KHB_HD uint64_t f9_shr29(uint64_t t) {
 #endif
 }
 
-// Columns c[0..16] of a product (c[k] = sum over i + j = k, each < 2^64) folded and normalised into
-// strict limbs.  High column k = 9 + j is split into its 32-bit halves: lo at limb k, and hi at
-// limb k (weight 2^(29k + 32)) = 8 * hi at limb k + 1; both are folded with 2^261 == 2^37 + 31264.
-KHB_HD void f9_reduce_cols(F9& r, uint64_t* c) {
-  uint64_t extra = 0;                                   // value at limb 9 left by the folds
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const uint32_t lo = (uint32_t)c[9 + j], hi = (uint32_t)(c[9 + j] >> 32);
-    f9_mad(c[j], lo, 31264u);                           // < 2^47
-    f9_mad(c[j + 1], lo, 256u);                         // < 2^40
-    f9_mad(c[j + 1], hi, 250112u);                      // 8 * 31264: < 2^50
-    if (j + 2 <= 8)
-      f9_mad(c[j + 2], hi, 2048u);                      // 8 * 256: < 2^43
-    else
-      extra = (uint64_t)hi * 2048u;                     // j = 7: hi of column 16 (< 2^29)
-  }
-  // normalise limbs 0..8; t ends as the value at limb 9 (< 2^36)
+// Fold the high column k = 9 + j (value h, < 2^64) into the low columns c[0..8] (and the value
+// left at limb 9, extra): h's lo word sits at limb k, its hi word at limb k (weight
+// 2^(29k + 32)) = 8 * hi at limb k + 1, and 2^261 == 2^37 + 31264 moves limb 9 + j to limbs j, j + 1.
+KHB_HD void f9_fold_col(uint64_t* c, uint64_t& extra, int j, uint64_t h, uint32_t k256, uint32_t k2048) {
+  const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+  f9_mad(c[j], lo, 31264u);                             // < 2^47
+  f9_mad(c[j + 1], lo, k256);                           // < 2^40
+  f9_mad(c[j + 1], hi, 250112u);                        // 8 * 31264: < 2^50
+  if (j + 2 <= 8)
+    f9_mad(c[j + 2], hi, k2048);                        // 8 * 256: < 2^43
+  else
+    extra = (uint64_t)hi * k2048;                       // j = 7: hi of column 16 (< 2^29)
+}
+
+// Normalise the folded low columns c[0..8] (each < 2^64) into strict limbs.
+KHB_HD void f9_normalize(F9& r, const uint64_t* c, uint64_t extra, uint32_t k256) {
+  // t ends as the value at limb 9 (< 2^36)
   uint64_t t = c[0];
   r.v[0] = (uint32_t)t & KHB_M29;
   t = f9_shr29(t);
@@ -95,42 +124,59 @@ KHB_HD void f9_reduce_cols(F9& r, uint64_t* c) {
   uint64_t t0 = r.v[0];
   f9_mad(t0, e9, 31264u);                               // < 2^45
   uint64_t t1 = r.v[1] + (t0 >> 29);
-  f9_mad(t1, e9, 256u);
+  f9_mad(t1, e9, k256);
   f9_mad(t1, e10, 31264u);                              // < 2^42
   r.v[0] = (uint32_t)t0 & KHB_M29;
   r.v[1] = (uint32_t)t1 & KHB_M29;
   r.v[2] += (uint32_t)(t1 >> 29) + e10 * 256u;          // < 2^13 + 2^19: limb 2 < 2^29 + 2^20
 }
 
-// r = a * b (mod p), strict limbs.
+// r = a * b (mod p), strict limbs.  The low columns are accumulated first and each high column
+// is folded as soon as it is complete, so at most one high column is live (register pressure).
 KHB_HD void f9_mul(F9& r, const F9& a, const F9& b) {
-  uint64_t c[17];
+  const uint32_t k256 = f9_k(256u), k2048 = f9_k(2048u);
+  uint64_t c[9], extra = 0;
 #pragma unroll
-  for (int k = 0; k < 17; ++k) {
-    const int lo = k > 8 ? k - 8 : 0, hi = k < 8 ? k : 8;
-    uint64_t s = (uint64_t)a.v[lo] * b.v[k - lo];
+  for (int k = 0; k < 9; ++k) {
+    uint64_t s = (uint64_t)a.v[0] * b.v[k];
 #pragma unroll
-    for (int i = lo + 1; i <= hi; ++i) s += (uint64_t)a.v[i] * b.v[k - i];
+    for (int i = 1; i <= k; ++i) s += (uint64_t)a.v[i] * b.v[k - i];
     c[k] = s;
   }
-  f9_reduce_cols(r, c);
+#pragma unroll
+  for (int k = 9; k < 17; ++k) {
+    f9_fence();
+    uint64_t s = (uint64_t)a.v[k - 8] * b.v[8];
+#pragma unroll
+    for (int i = k - 7; i <= 8; ++i) s += (uint64_t)a.v[i] * b.v[k - i];
+    f9_fold_col(c, extra, k - 9, s, k256, k2048);
+  }
+  f9_fence();
+  f9_normalize(r, c, extra, k256);
 }
 
-// r = a^2 (mod p): cross products against the doubled operand, 45 products.
+// r = a^2 (mod p): cross products against the doubled operand, 45 products; high columns folded
+// as they complete (f9_mul).
 KHB_HD void f9_sqr(F9& r, const F9& a) {
+  const uint32_t k256 = f9_k(256u), k2048 = f9_k(2048u);
   uint32_t d[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;      // < 2^31.4
-  uint64_t c[17];
+  uint64_t c[9], extra = 0;
 #pragma unroll
   for (int k = 0; k < 17; ++k) {
     const int lo = k > 8 ? k - 8 : 0;
     uint64_t s = (k & 1) ? 0 : (uint64_t)a.v[k >> 1] * a.v[k >> 1];
 #pragma unroll
     for (int i = lo; 2 * i < k; ++i) s += (uint64_t)a.v[i] * d[k - i];
-    c[k] = s;
+    if (k < 9) {
+      c[k] = s;
+    } else {
+      f9_fold_col(c, extra, k - 9, s, k256, k2048);
+      f9_fence();
+    }
   }
-  f9_reduce_cols(r, c);
+  f9_normalize(r, c, extra, k256);
 }
 
 KHB_HD void f9_sqr_n(F9& r, const F9& a, int n) {

@@ -104,6 +104,23 @@ int main() {
       if (!same(ve, vg)) { if (fails++ < 10) printf("FAIL inv it %d\n", it); }
     }
   }
+  // a + 2p - b (f9_add_neg) for canonical b, and its product with a strict value
+  for (int it = 0; it < 50000; ++it) {
+    const F9 a = (it & 1) ? rnd_canon(it % 3) : rnd_f9(1, 1.0);      // strict or limbs at 2^30 - 256
+    const F9 b = rnd_canon(it % 3 == 1 ? 1 : 0);
+    F9 d, m, q;
+    f9_add_neg(d, a, b);
+    ora_u256 va, vb, vd, ve, vm;
+    f9_value(&va, a); f9_value(&vb, b); f9_value(&vd, d);
+    ora_fe_sub(&ve, &va, &vb);
+    if (!same(ve, vd)) { if (fails++ < 10) printf("FAIL add_neg it %d\n", it); }
+    f9_mul(q, rnd_canon(0), rnd_canon(2));                            // a strict product result
+    f9_mul(m, d, q);
+    ora_u256 vq; f9_value(&vq, q);
+    ora_fe_mul_exact(&ve, &vd, &vq);
+    f9_value(&vm, m);
+    if (!same(ve, vm)) { if (fails++ < 10) printf("FAIL add_neg product it %d\n", it); }
+  }
   // the gate's rare flag: limb 8 within 4 of a multiple of 2^24 (and its exact neighbours)
   for (int it = 0; it < 20000; ++it) {
     F9 g = rnd_f9(0, 1.0);

@@ -37,14 +37,18 @@ template <int OP>
 __global__ __launch_bounds__(256) void k_tp(const Fe* seed, Fe* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   Fe x = seed[i & 1023], y = seed[(i + 7) & 1023];
-  F9 u, v;
+  F9 u, v, u2;
   f9_from_fe(u, x); f9_from_fe(v, y);
+  const Fe x2 = seed[(i + 3) & 1023];
+  f9_from_fe(u2, x2);
   for (int it = 0; it < ITERS; ++it) {
     if (OP == 0) fm_mul(x, x, y);
     if (OP == 1) fm_sqr(x, x);
     if (OP == 2) f9_mul(u, u, v);
     if (OP == 3) f9_sqr(u, u);
     if (OP == 4) { uint32_t w0, w1; bool r; f9_gate_words(w0, w1, r, u); u.v[0] ^= w0 ^ w1 ^ (r ? 1u : 0u); }
+    if (OP == 6) { fm_mul(x, x, y); fm_mul(y, y, x2); }
+    if (OP == 7) { f9_mul(u, u, v); f9_mul(v, v, u2); }
     if (OP == 5) {   // raw v_lshrrev_b64 rate, 8 independent chains
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -54,12 +58,13 @@ __global__ __launch_bounds__(256) void k_tp(const Fe* seed, Fe* out) {
       }
     }
   }
-  if (OP >= 2) for (int k = 0; k < 8; ++k) x.v[k] = (u.v[k] * 0x9E3779B1u) ^ u.v[8];
+  if (OP >= 2 && OP != 6) for (int k = 0; k < 8; ++k) x.v[k] = (u.v[k] * 0x9E3779B1u) ^ u.v[8] ^ v.v[k];
+  if (OP == 6) for (int k = 0; k < 8; ++k) x.v[k] ^= y.v[k];
   if (x.v[0] == 0x12345678u && x.v[1] == 0x9abcdef0u) out[i] = x;
 }
 
 const char* names[] = {"fm_mul (8x32 asm)", "fm_sqr (8x32 asm)", "f9_mul (9x29)", "f9_sqr (9x29)", "f9_gate_words",
-                       "8x (v_lshrrev_b64+xor)"};
+                       "8x (v_lshrrev_b64+xor)", "2 fm_mul chains (x2 ops)", "2 f9_mul chains (x2 ops)"};
 
 template <int OP>
 int run(const Fe* seed, Fe* out, int cus) {
@@ -100,7 +105,7 @@ int main() {
   printf("exactness over %d inputs: %s (mask 0x%x: 1 mul 2 sqr 4 gate words)\n", n, bad ? "MISMATCH" : "ok", bad);
   Fe* dout; CHECK(hipMalloc(&dout, (size_t)cus * 1024 * sizeof(Fe)));
   if (run<0>(da, dout, cus) || run<1>(da, dout, cus) || run<2>(da, dout, cus) || run<3>(da, dout, cus) ||
-      run<4>(da, dout, cus) || run<5>(da, dout, cus))
+      run<4>(da, dout, cus) || run<5>(da, dout, cus) || run<6>(da, dout, cus) || run<7>(da, dout, cus))
     return 1;
   return bad ? 2 : 0;
 }
