@@ -30,6 +30,14 @@ fmax = max(fetch.values())
 f_full = [v for v in fetch.values() if v > 0.9 * fmax]
 w_full = sorted(write.values())[-len(f_full):]
 f_kib, w_kib = statistics.mean(f_full), statistics.mean(w_full)
+valu_path = os.path.join(d, "valu", "valu_counter_collection.csv")
+valu = {}
+if os.path.exists(valu_path):
+    for cn in ("SQ_INSTS_VALU", "VALUBusy", "OccupancyPercent"):
+        v = per_dispatch(valu_path, cn)
+        vmax = max(v.values()) if v else 0
+        full = [x for x in v.values() if x > 0.9 * vmax] if cn == "SQ_INSTS_VALU" else list(v.values())
+        valu[cn] = statistics.mean(full) if full else None
 stats = list(csv.DictReader(open(os.path.join(d, "trace", "trace_kernel_stats.csv"))))
 scan = [r for r in stats if "k_giant_scan" in r["Name"]]
 out = {
@@ -43,6 +51,10 @@ out = {
     "hbm_bytes_per_launch": int((f_kib + w_kib) * 1024),
     "bytes_per_giant_step": round((f_kib + w_kib) * 1024 / steps_per_launch, 2),
     "trace_avg_ns": float(scan[0]["AverageNs"]) if scan else None,
+    "valu_instr_per_giant_step": round(valu["SQ_INSTS_VALU"] * 64 / steps_per_launch, 1) if valu.get("SQ_INSTS_VALU") else None,
+    "valu_busy_pct": round(valu["VALUBusy"], 2) if valu.get("VALUBusy") else None,
+    "occupancy_pct": round(valu["OccupancyPercent"], 2) if valu.get("OccupancyPercent") else None,
+    "valu_source": os.path.relpath(valu_path, REPO) if valu else None,
     "note": "FETCH_SIZE+WRITE_SIZE (KiB) x 1024 per full-size dispatch, uncorrected: the access mix "
             "(1-B random bloom probes, 16-B scratch streams, LDS-free spills) has no gfx950 calibration, and "
             "FETCH_SIZE counts Infinity-Cache hits (MI355X_MICROARCH.md HBM section)",

@@ -11,7 +11,8 @@ B="--steps 5 --warmup 1 --no-cpu-baseline $*"
 timeout -k 10 600 python3 bench.py $* > $OUT/bench.json 2> $OUT/bench.err && \
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- python3 bench.py $B > $OUT/trace.log 2>&1 && \
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o fetch --output-format csv -- python3 bench.py $B > $OUT/fetch.log 2>&1 && \
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o write --output-format csv -- python3 bench.py $B > $OUT/write.log 2>&1
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o write --output-format csv -- python3 bench.py $B > $OUT/write.log 2>&1 && \
+timeout -k 10 400 rocprofv3 --pmc VALUBusy SQ_INSTS_VALU OccupancyPercent -d $OUT/valu -o valu --output-format csv -- python3 bench.py $B > $OUT/valu.log 2>&1
 rc=$?
 cat $OUT/bench.json
 echo "rc=$rc"
