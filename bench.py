@@ -139,7 +139,16 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # gloo's C++ connect messages go to fd 1; keep stdout for the one JSON line (rank 0)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.barrier()
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
 
     from keyhuntm1cpu_amd import khhost
     from keyhuntm1cpu_amd.partition import rank_range
