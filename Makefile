@@ -128,3 +128,6 @@ $(LIBDIR)/variants/libkhbsgs_f9w%.so: $(HIP_SRCS) $(DEV_HDRS)
 $(LIBDIR)/variants/libkhbsgs_cnv%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) -DKHB_CN_VOLATILE=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/libkhbsgs_gs%.so: $(HIP_SRCS) $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants
+	$(HIPCC) $(HIPFLAGS) -DKHB_GATE_SHR64=$* -shared -o $@ $(HIP_SRCS)

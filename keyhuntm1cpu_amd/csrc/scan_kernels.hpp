@@ -258,8 +258,19 @@ __device__ __forceinline__ uint32_t gate_bits(const ScanArgs& A, const Fe& x) {
   return b0 | (b1 << 6) | (b2 << 12);
 }
 
-// All three packed bits set in the 64-bit block (lo, hi)?
+// All three packed bits set in the 64-bit block (lo, hi)?  KHB_GATE_SHR64: one 64-bit shift per bit
+// (v_lshrrev_b64) instead of a word select and a 32-bit shift: 28 instead of 38 VALU per walk step,
+// measured no faster (47.39 vs 47.54 G steps/s, profiles/r02p_gate_shr64_ab.txt), so off.
+#ifndef KHB_GATE_SHR64
+#define KHB_GATE_SHR64 0
+#endif
 __device__ __forceinline__ bool gate_block_pass(uint32_t lo, uint32_t hi, uint32_t bits) {
+#if KHB_GATE_SHR64
+  const uint64_t blk = ((uint64_t)hi << 32) | lo;
+  const uint32_t r = (uint32_t)(blk >> (bits & 63u)) & (uint32_t)(blk >> ((bits >> 6) & 63u)) &
+                     (uint32_t)(blk >> ((bits >> 12) & 63u));
+  return r & 1u;
+#else
   uint32_t r = 1u;
 #pragma unroll
   for (int p = 0; p < 3; ++p) {
@@ -267,6 +278,7 @@ __device__ __forceinline__ bool gate_block_pass(uint32_t lo, uint32_t hi, uint32
     r &= ((b & 32u) ? hi : lo) >> (b & 31u);
   }
   return r & 1u;
+#endif
 }
 
 // A gate test: x's 64-bit block of the map (one 8-byte load: a single cache line per x whatever
@@ -1076,6 +1088,9 @@ __device__ __forceinline__ void x_dump9(const ScanArgs& A, const F9& x, uint32_t
 #ifndef KHB_CN_VOLATILE
 #define KHB_CN_VOLATILE 1
 #endif
+#ifndef KHB_CN_LDS
+#define KHB_CN_LDS 1              // F9 walk: p - C.x and C.y parked in LDS (0: held in registers)
+#endif
 __device__ __forceinline__ F9 cn_load(const ProbeQueue& Q, int which) {
   uint32_t wl = threadIdx.x & 63u;
   F9 r;
@@ -1099,6 +1114,7 @@ __device__ __forceinline__ void walk_group_g9(const ScanArgs& A, ProbeQueue& Q, 
   constexpr bool STAGE1 = MODE == kScanG1;
   const Gsn9 g9{A.gsn9};
   const uint32_t base = j * KHB_GROUP;
+#if KHB_CN_LDS
   {
     Fe p, t;
     F9 ncx, cy;
@@ -1116,6 +1132,17 @@ __device__ __forceinline__ void walk_group_g9(const ScanArgs& A, ProbeQueue& Q, 
   }
 #define ncx cn_load(Q, 0)
 #define cy cn_load(Q, 1)
+#else
+  F9 ncx, cy;
+  {
+    Fe p, t;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p.v[k] = k == 0 ? KHB_P0 : (k == 1 ? KHB_P1 : 0xFFFFFFFFu);
+    fm_sub(t, p, C.x);
+    f9_from_fe(ncx, t);
+    f9_from_fe(cy, C.y);
+  }
+#endif
   F9 pre = sg.ld9(e0 + kHalf - 2);
   F9 idx, dx, s, x;
   {   // step 511: pts[0] = C - GSn[511] only
@@ -1206,8 +1233,10 @@ __device__ __forceinline__ void walk_group_g9(const ScanArgs& A, ProbeQueue& Q, 
       }
     }
   }
+#if KHB_CN_LDS
 #undef ncx
 #undef cy
+#endif
   if constexpr (MODE == kDumpG) {
     fe_to_be(A.xdump + ((uint64_t)(j - A.group_begin) * KHB_GROUP + kHalf) * 32, C.x);
   } else {
