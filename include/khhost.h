@@ -51,6 +51,11 @@ const uint8_t* khh_bptable(const khh_tables* t, uint64_t* n);
 
 /* startP of (chunk base, target): keyhunt.cpp:3861-3869 */
 int khh_chunk_centre(const khh_tables* t, const uint8_t base_be[32], const uint8_t target_xy[64], uint8_t out_xy[64]);
+/* The search engine's batched centres (engine.cpp job_centres) of n_chunks x n_targets jobs:
+ * out[64 * (c * n_targets + j)] = centre of chunk bases[c] for target j (what khh_chunk_centre gives
+ * one at a time); consecutive bases (2N apart) take the batched auxiliary walk. */
+int khh_job_centres(const khh_tables* t, const uint8_t* bases_be, uint32_t n_chunks, const uint8_t* targets_xy,
+                    uint32_t n_targets, uint8_t* out_xy, int threads);
 /* bsgs_secondcheck: 1 found (key_be filled), 0 not found */
 int khh_secondcheck(const khh_tables* t, const uint8_t base_be[32], uint32_t a, const uint8_t target_xy[64],
                     uint8_t key_be[32]);

@@ -391,6 +391,64 @@ void batch_add_direct(const Pt* targets, const Pt& aux, size_t n, Pt* out) {
   }
 }
 
+// out[i] = AddDirect(a[i], b[i]) for i < n with one shared inversion (SECP256K1.cpp:242-265
+// semantics per element: a zero x-difference gets inverse 0, as batch_add_direct).
+void batch_add_pairs(const Pt* a, const Pt* b, size_t n, Pt* out) {
+  std::vector<Fh> dx(n), pre(n);
+  for (size_t k = 0; k < n; ++k) fe_sub(dx[k], b[k].x, a[k].x);
+  fe_batch_inv(dx.data(), n, pre.data());
+  for (size_t k = 0; k < n; ++k) {
+    Fh dy, s, p;
+    Pt r;
+    fe_sub(dy, b[k].y, a[k].y);
+    fe_mul(s, dy, dx[k]);
+    fe_sqr(p, s);
+    fe_sub(r.x, p, a[k].x);
+    fe_sub(r.x, r.x, b[k].x);
+    fe_sub(r.y, b[k].x, r.x);
+    fe_mul(r.y, r.y, s);
+    fe_sub(r.y, r.y, b[k].y);
+    out[k] = r;
+  }
+}
+
+// Chunk auxiliaries aux(base_c) = (order - base_c - intaux) G (keyhunt.cpp:3861-3866) for
+// base_c = base0 + c * 2N, c < n: one scalar multiplication per block of kAuxBlock chunks, the rest
+// aux(block start) - j * 2N G by batched affine additions (one inversion per block).  A degenerate
+// addition (aux(block start) = +-j * 2N G) falls back to the scalar multiplication.
+void Tables::chunk_aux_run(const U256& base0, size_t n, Pt* aux, int threads) const {
+  constexpr size_t kAuxBlock = 64;
+  if (n == 0) return;
+  const Pt D = mul_g(secp_order() - geo.N_double);          // -(2N) G
+  std::vector<Pt> jd(kAuxBlock);                             // jd[j] = j * D, j >= 1
+  jd[1] = D;
+  jd[2] = mul_g(secp_order() - geo.N_double * 2ull);         // not D + D: AddDirect cannot double
+  for (size_t j = 3; j < kAuxBlock; ++j) jd[j] = add_direct(jd[j - 1], D);
+  const size_t blocks = (n + kAuxBlock - 1) / kAuxBlock;
+  auto body = [&](size_t blk) {
+    const size_t s = blk * kAuxBlock, m = std::min(kAuxBlock, n - s);
+    const U256 bs = base0 + geo.N_double * (uint64_t)s;
+    aux[s] = chunk_aux(bs);
+    if (m < 2) return;
+    std::vector<Pt> a(m - 1, aux[s]);
+    batch_add_pairs(a.data(), jd.data() + 1, m - 1, aux + s + 1);
+    for (size_t j = 1; j < m; ++j)
+      if (fe_eq(aux[s].x, jd[j].x)) aux[s + j] = chunk_aux(bs + geo.N_double * (uint64_t)j);
+  };
+  if (threads <= 1 || blocks < 2) {
+    for (size_t b = 0; b < blocks; ++b) body(b);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  auto worker = [&]() {
+    for (size_t b; (b = next.fetch_add(1)) < blocks;) body(b);
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads && (size_t)t < blocks; ++t) th.emplace_back(worker);
+  worker();
+  for (auto& t : th) t.join();
+}
+
 bool Tables::searchbinary(const uint8_t* x, uint64_t& idx) const {
   // bsgs_searchbinary (keyhunt.cpp:3748-3773): probes bytes 16..21 of x
   int64_t lo = 0, hi = (int64_t)bp.size() - 1;

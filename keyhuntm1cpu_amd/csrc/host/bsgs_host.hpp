@@ -82,6 +82,8 @@ struct Tables {
 
   // (order - base - intaux) * G, shared by every target of a chunk (keyhunt.cpp:3862-3866)
   Pt chunk_aux(const U256& base) const;
+  // chunk_aux of n consecutive chunks base0 + c * 2N, batched (one scalar multiplication per 64)
+  void chunk_aux_run(const U256& base0, size_t n, Pt* aux, int threads) const;
   bool secondcheck(const U256& base, uint32_t a, const Pt& target, U256& key) const;
 
  private:
@@ -91,5 +93,7 @@ struct Tables {
 
 // Batched chunk centres: out[k] = AddDirect(targets[k], aux) with one shared inversion.
 void batch_add_direct(const Pt* targets, const Pt& aux, size_t n, Pt* out);
+// out[i] = AddDirect(a[i], b[i]) with one shared inversion
+void batch_add_pairs(const Pt* a, const Pt* b, size_t n, Pt* out);
 
 }  // namespace khb

@@ -85,7 +85,11 @@ bool claim(Shared& S, uint32_t want, Batch& b) {
   return !b.bases.empty();
 }
 
-// Centres of every (chunk, live target) job: target + (order - base - intaux)*G.
+// Centres of every (chunk, live target) job: target + (order - base - intaux)*G
+// (keyhunt.cpp:3861-3869).  Sequential chunks (bases 2N apart) take their auxiliary points from a
+// batched walk (Tables::chunk_aux_run: one scalar multiplication per 64 chunks) instead of one
+// scalar multiplication each, and the job additions share one inversion per block of 256 jobs
+// across chunks: at small -n (few groups per chunk) the host would otherwise set the pace.
 void make_jobs(Shared& S, Batch& b, int threads) {
   std::vector<int> live;
   {
@@ -97,20 +101,44 @@ void make_jobs(Shared& S, Batch& b, int threads) {
   b.job_chunk.resize(nc * nt);
   b.job_target.resize(nc * nt);
   b.centres.resize(64 * nc * nt);
+  if (nc == 0 || nt == 0) return;
   std::vector<Pt> tp(nt);
   for (size_t j = 0; j < nt; ++j) tp[j] = S.targets[live[j]].p;
-  parallel_for(nc, threads, [&](size_t c) {
-    const Pt aux = S.T.chunk_aux(b.bases[c]);
-    std::vector<Pt> out(nt);
-    batch_add_direct(tp.data(), aux, nt, out.data());
-    for (size_t j = 0; j < nt; ++j) {
-      const size_t job = c * nt + j;
-      b.job_chunk[job] = (uint32_t)c;
-      b.job_target[job] = (uint32_t)live[j];
-      pt_to_be(b.centres.data() + 64 * job, out[j]);
+  for (size_t job = 0; job < nc * nt; ++job) {
+    b.job_chunk[job] = (uint32_t)(job / nt);
+    b.job_target[job] = (uint32_t)live[job % nt];
+  }
+  job_centres(S.T, b.bases, tp, b.centres.data(), threads);
+}
+
+}  // namespace
+
+void job_centres(const Tables& T, const std::vector<U256>& bases, const std::vector<Pt>& tp, uint8_t* out,
+                 int threads) {
+  const size_t nc = bases.size(), nt = tp.size();
+  if (nc == 0 || nt == 0) return;
+  std::vector<Pt> aux(nc);
+  bool consecutive = nc > 1;
+  for (size_t c = 1; c < nc && consecutive; ++c) consecutive = bases[c] == bases[c - 1] + T.geo.N_double;
+  if (consecutive)
+    T.chunk_aux_run(bases[0], nc, aux.data(), threads);
+  else
+    parallel_for(nc, threads, [&](size_t c) { aux[c] = T.chunk_aux(bases[c]); });
+  constexpr size_t kJobBlock = 256;
+  const size_t nj = nc * nt;
+  parallel_for((nj + kJobBlock - 1) / kJobBlock, threads, [&](size_t blk) {
+    const size_t s0 = blk * kJobBlock, m = std::min(kJobBlock, nj - s0);
+    std::vector<Pt> ta(m), xa(m), res(m);
+    for (size_t i = 0; i < m; ++i) {
+      ta[i] = tp[(s0 + i) % nt];
+      xa[i] = aux[(s0 + i) / nt];
     }
+    batch_add_pairs(ta.data(), xa.data(), m, res.data());
+    for (size_t i = 0; i < m; ++i) pt_to_be(out + 64 * (s0 + i), res[i]);
   });
 }
+
+namespace {
 
 // Confirm level-1 candidates (bsgs_secondcheck, keyhunt.cpp:3947-3982): speculative parallel
 // checks, then in-order resolution.

@@ -21,6 +21,11 @@ struct Target {
   bool compressed = true;
 };
 
+// Centres of the jobs (chunk c, target j) -> out[64 * (c * nt + j)], x||y big-endian:
+// tp[j] + (order - bases[c] - intaux) G (keyhunt.cpp:3861-3869), batched (engine.cpp).
+void job_centres(const Tables& T, const std::vector<U256>& bases, const std::vector<Pt>& tp, uint8_t* out,
+                 int threads);
+
 struct SearchConfig {
   std::vector<int> devices{0};
   uint32_t lanes = 0;              // per device, 0 = library default

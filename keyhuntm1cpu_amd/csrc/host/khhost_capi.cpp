@@ -3,6 +3,7 @@
 
 #include <string>
 #include <thread>
+#include <vector>
 
 #include "../../../include/khbsgs.h"
 #include "../../../include/khhost.h"
@@ -146,6 +147,17 @@ int khh_chunk_centre(const khh_tables* t, const uint8_t base_be[32], const uint8
   Pt c;
   batch_add_direct(&tg, aux, 1, &c);
   pt_to_be(out_xy, c);
+  return 0;
+}
+
+int khh_job_centres(const khh_tables* t, const uint8_t* bases_be, uint32_t n_chunks, const uint8_t* targets_xy,
+                    uint32_t n_targets, uint8_t* out_xy, int threads) {
+  if (!t || !bases_be || !targets_xy || !out_xy) return -1;
+  std::vector<U256> bases(n_chunks);
+  for (uint32_t c = 0; c < n_chunks; ++c) bases[c] = U256::from_be(bases_be + 32 * (size_t)c);
+  std::vector<Pt> tp(n_targets);
+  for (uint32_t j = 0; j < n_targets; ++j) tp[j] = pt_from_be(targets_xy + 64 * (size_t)j);
+  job_centres(t->t, bases, tp, out_xy, threads);
   return 0;
 }
 

@@ -47,6 +47,7 @@ def lib() -> C.CDLL:
         L.khh_gate_probes.restype = C.c_uint32
         L.khh_gate_probes.argtypes = [C.c_void_p]
         L.khh_chunk_centre.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p]
+        L.khh_job_centres.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_char_p, C.c_int]
         L.khh_secondcheck.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_char_p, C.c_char_p]
         L.khh_search.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, P(C.c_int), C.c_int,
                                  C.c_uint32, C.c_uint32, C.c_uint64, P(C.c_int), C.c_char_p, P(C.c_uint64),
@@ -190,6 +191,13 @@ class Tables:
     def chunk_centre(self, base: int, target_xy: bytes) -> bytes:
         out = C.create_string_buffer(64)
         lib().khh_chunk_centre(self.h, _b32(base), target_xy, out)
+        return out.raw
+
+    def job_centres(self, bases: list[int], targets_xy: list[bytes], threads: int = 8) -> bytes:
+        """The engine's batched centres of every (chunk, target) job, chunk-major (khh_job_centres)."""
+        out = C.create_string_buffer(64 * len(bases) * len(targets_xy))
+        lib().khh_job_centres(self.h, b"".join(_b32(b) for b in bases), len(bases), b"".join(targets_xy),
+                              len(targets_xy), out, threads)
         return out.raw
 
     def secondcheck(self, base: int, a: int, target_xy: bytes) -> int | None:

@@ -106,3 +106,27 @@ def test_level0_gate_exact(pair, ora):
         for b in gate_bits(lg, probes, x):
             exp[b >> 3] |= 1 << (b & 7)
     assert gate == bytes(exp)
+
+
+def test_batched_job_centres(ora):
+    """The engine's batched centres (khh_job_centres: one scalar multiplication per 64 consecutive
+    chunks, job additions sharing inversions across chunks) equal the per-chunk centres and the
+    oracle's chunk start (keyhunt.cpp:3861-3869): consecutive runs crossing block boundaries, a run
+    whose first auxiliary point equals 5 * (-2N G) (the doubling fallback), and random bases."""
+    import random
+    t = khhost.Tables("0x1000000", 1, threads=4)
+    o = ora.Bsgs("0x1000000", 1, 4)
+    two_n = 2 * t.n_low
+    intaux = 2 * t.m * 512 + t.m
+    tg = [khhost.pubkey(0x123456789 + 77 * i) for i in range(3)]
+    rng = random.Random(7)
+    runs = [[(1 << 40) + c * two_n for c in range(200)],
+            [5 * two_n - intaux + c * two_n for c in range(70)],
+            [rng.randrange(1, 1 << 250) for _ in range(40)]]
+    for bases in runs:
+        got = t.job_centres(bases, tg)
+        assert got == b"".join(t.chunk_centre(b, x) for b in bases for x in tg)
+    out = t.job_centres(runs[0], tg)
+    target0 = ora.parse_pubkey("04" + tg[0].hex())[0]
+    for c in range(60, 70):
+        assert out[64 * 3 * c:64 * 3 * c + 64] == o.chunk_start(runs[0][c], target0).be64()
