@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <deque>
 #include <thread>
 
 #include "../../../include/khbsgs.h"
@@ -359,62 +360,95 @@ void device_loop(AddrShared& S, int device) {
   }
   const uint64_t lanes_per_job = (groups + S.G.gpl - 1) / S.G.gpl;
   const uint64_t lanes = khb_lanes(ctx);
-  uint64_t per_batch = (2 * lanes + lanes_per_job - 1) / lanes_per_job;
+  // about eight work items per lane (the kernel's waves take items dynamically, so a deep launch
+  // keeps every SIMD full until its last items), and two launches queued (the context's two
+  // submission slots): the next launch fills the CUs the current one's tail leaves idle
+  uint64_t per_batch = (8 * lanes + lanes_per_job - 1) / lanes_per_job;
   if (per_batch < 1) per_batch = 1;
   if (per_batch > 4096) per_batch = 4096;
-  std::vector<khb_addr_hit> hits(1u << 18);
-  const U256 half = S.G.stride * 512u;
-  for (;;) {
-    if (S.cb.stop && S.cb.stop()) break;
+  struct ABatch {
     std::vector<U256> bases;
+    std::vector<uint8_t> centres;
+  };
+  ABatch ring[3];
+  int next = 0;
+  auto take = [&]() { const int i = next; next = (next + 1) % 3; return i; };
+  const U256 half = S.G.stride * 512u;
+  auto prepare = [&](ABatch& b) {
+    b.bases.clear();
+    if (S.cb.stop && S.cb.stop()) return false;
     {
       std::lock_guard<std::mutex> lk(S.mu);
-      if (S.rc) break;
-      while (bases.size() < per_batch) {
+      if (S.rc) return false;
+      while (b.bases.size() < per_batch) {
         if (S.cfg.max_chunks && S.claimed >= S.cfg.max_chunks) break;
         if (S.cfg.random) {
-          bases.push_back(random_in(S.cfg.start, S.cfg.end));
+          b.bases.push_back(random_in(S.cfg.start, S.cfg.end));
         } else {
           if (!(S.cursor < S.cfg.end)) break;
-          bases.push_back(S.cursor);
+          b.bases.push_back(S.cursor);
           S.cursor = S.cursor + U256(S.cfg.n_seq);
         }
         ++S.claimed;
       }
     }
-    if (bases.empty()) break;
+    if (b.bases.empty()) return false;
     if (S.cb.on_chunk)
-      for (const U256& b : bases) S.cb.on_chunk(b, device);
-    std::vector<uint8_t> centres(64 * bases.size());
-    for (size_t k = 0; k < bases.size(); ++k) {
-      U256 c = bases[k] + half, r;   // startP = ComputePublicKey(key_mpz + 512*stride)
+      for (const U256& c : b.bases) S.cb.on_chunk(c, device);
+    b.centres.resize(64 * b.bases.size());
+    for (size_t k = 0; k < b.bases.size(); ++k) {
+      U256 c = b.bases[k] + half, r;   // startP = ComputePublicKey(key_mpz + 512*stride)
       U256::divmod(c, secp_order(), nullptr, &r);
-      pt_to_be(centres.data() + 64 * k, mul_g(r));
+      pt_to_be(b.centres.data() + 64 * k, mul_g(r));
     }
+    return true;
+  };
+  auto submit = [&](ABatch& b) {
+    return khb_addr_submit(ctx, b.centres.data(), (uint32_t)b.bases.size(), 0, groups, S.cfg.search);
+  };
+  std::vector<khb_addr_hit> hits(1u << 18);
+  std::deque<int> q;
+  while (q.size() < 2) {
+    const int i = take();
+    if (!prepare(ring[i])) break;
+    if ((rc = submit(ring[i]))) { fail(rc, "khb_addr_submit"); break; }
+    q.push_back(i);
+  }
+  int pre = -1;
+  while (!q.empty()) {
+    if (pre < 0 && !rc) {
+      const int k = take();
+      if (prepare(ring[k])) pre = k;                  // overlaps the GPU scan
+    }
+    const int i = q.front();
+    q.pop_front();
     khb_stats st{};
-    rc = khb_addr_scan(ctx, centres.data(), (uint32_t)bases.size(), 0, groups, S.cfg.search, hits.data(),
-                       (uint32_t)hits.size(), &st);
-    if (rc) {
-      fail(rc, "khb_addr_scan");
-      break;
+    const int crc = khb_addr_collect(ctx, hits.data(), (uint32_t)hits.size(), &st);
+    if (crc) { fail(crc, "khb_addr_collect"); rc = crc; continue; }   // keep draining the queue
+    if (pre >= 0 && !rc) {
+      if ((rc = submit(ring[pre]))) fail(rc, "khb_addr_submit");
+      else q.push_back(pre);
     }
+    pre = -1;
+    if (rc) continue;
+    const ABatch& b = ring[i];
     const uint32_t nh = st.n_cand < hits.size() ? st.n_cand : (uint32_t)hits.size();
-    std::sort(hits.begin(), hits.begin() + nh, [](const khb_addr_hit& a, const khb_addr_hit& b) {
-      if (a.job != b.job) return a.job < b.job;
-      if (a.group != b.group) return a.group < b.group;
-      if (a.t != b.t) return a.t < b.t;
-      return a.kind < b.kind;
+    std::sort(hits.begin(), hits.begin() + nh, [](const khb_addr_hit& x, const khb_addr_hit& y) {
+      if (x.job != y.job) return x.job < y.job;
+      if (x.group != y.group) return x.group < y.group;
+      if (x.t != y.t) return x.t < y.t;
+      return x.kind < y.kind;
     });
     std::vector<AddrFound> found;
-    for (uint32_t i = 0; i < nh; ++i) {
-      const khb_addr_hit& h = hits[i];
-      const U256 key = bases[h.job] + S.G.stride * ((uint64_t)h.group * 1024u + h.t);
+    for (uint32_t h = 0; h < nh; ++h) {
+      const khb_addr_hit& ht = hits[h];
+      const U256 key = b.bases[ht.job] + S.G.stride * ((uint64_t)ht.group * 1024u + ht.t);
       AddrFound f;
-      if (confirm_hit(S.T, key, h.kind, &f)) found.push_back(f);
+      if (confirm_hit(S.T, key, ht.kind, &f)) found.push_back(f);
     }
     std::lock_guard<std::mutex> lk(S.mu);
     S.stats.launches++;
-    S.stats.chunks += bases.size();
+    S.stats.chunks += b.bases.size();
     S.stats.keys += st.giant_steps;
     S.stats.hits += st.n_cand;
     S.stats.degenerate += st.n_degenerate;
