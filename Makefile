@@ -131,3 +131,7 @@ $(LIBDIR)/variants/libkhbsgs_cnv%.so: $(HIP_SRCS) $(DEV_HDRS)
 $(LIBDIR)/variants/libkhbsgs_gs%.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) -DKHB_GATE_SHR64=$* -shared -o $@ $(HIP_SRCS)
+# -m address occupancy A/B: a whole libkhbsgs.so per setting, swapped in with LD_LIBRARY_PATH
+$(LIBDIR)/variants/aw%/libkhbsgs.so: $(HIP_SRCS) $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants/aw$*
+	$(HIPCC) $(HIPFLAGS) -DKHB_ADDR_WAVES_PER_SIMD=$* -shared -o $@ $(HIP_SRCS)

@@ -17,8 +17,37 @@
 
 namespace khb {
 
-KHB_HD uint32_t ror32(uint32_t x, int r) { return (x >> r) | (x << (32 - r)); }
-KHB_HD uint32_t rol32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+// Rotates and three-input boolean functions.  On gfx950 a rotate is one v_alignbit_b32 and any
+// three-input boolean function is one v_bitop3_b32 (the 8-bit truth table over x = 0xF0, y = 0xCC,
+// z = 0xAA); the compiler forms bitop3 for ch/maj but not for the xor-of-rotates in the SHA-256
+// sigmas nor alignbit for RIPEMD-160's left rotates, so they are spelled out (VALU per SHA-256
+// block 1690 -> ~1450, RIPEMD-160 1153 -> ~1000).  The host build keeps the plain C expressions.
+KHB_HD uint32_t ror32(uint32_t x, int r) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_amdgcn_alignbit(x, x, (uint32_t)r);
+#else
+  return (x >> r) | (x << (32 - r));
+#endif
+}
+KHB_HD uint32_t rol32(uint32_t x, int r) { return ror32(x, 32 - r); }
+template <uint32_t TT>
+KHB_HD uint32_t bitop3(uint32_t x, uint32_t y, uint32_t z) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_amdgcn_bitop3_b32(x, y, z, TT);
+#else
+  uint32_t r = 0;
+  if (TT & 0x01u) r |= ~x & ~y & ~z;
+  if (TT & 0x02u) r |= ~x & ~y & z;
+  if (TT & 0x04u) r |= ~x & y & ~z;
+  if (TT & 0x08u) r |= ~x & y & z;
+  if (TT & 0x10u) r |= x & ~y & ~z;
+  if (TT & 0x20u) r |= x & ~y & z;
+  if (TT & 0x40u) r |= x & y & ~z;
+  if (TT & 0x80u) r |= x & y & z;
+  return r;
+#endif
+}
+KHB_HD uint32_t xor3(uint32_t x, uint32_t y, uint32_t z) { return bitop3<0x96u>(x, y, z); }
 
 // ---- SHA-256 (FIPS 180-4 §6.2) ----
 #define KHB_SHA_K                                                                                            \
@@ -47,15 +76,15 @@ KHB_HD void sha256_block(uint32_t s[8], uint32_t w[16]) {
       wi = w[i];
     } else {
       const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      const uint32_t s0 = ror32(w15, 7) ^ ror32(w15, 18) ^ (w15 >> 3);
-      const uint32_t s1 = ror32(w2, 17) ^ ror32(w2, 19) ^ (w2 >> 10);
+      const uint32_t s0 = xor3(ror32(w15, 7), ror32(w15, 18), w15 >> 3);
+      const uint32_t s1 = xor3(ror32(w2, 17), ror32(w2, 19), w2 >> 10);
       wi = w[i & 15] = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
     }
-    const uint32_t S1 = ror32(e, 6) ^ ror32(e, 11) ^ ror32(e, 25);
-    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t S1 = xor3(ror32(e, 6), ror32(e, 11), ror32(e, 25));
+    const uint32_t ch = bitop3<0xCAu>(e, f, g);                  // (e & f) ^ (~e & g)
     const uint32_t t1 = h + S1 + ch + K[i] + wi;
-    const uint32_t S0 = ror32(a, 2) ^ ror32(a, 13) ^ ror32(a, 22);
-    const uint32_t maj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t S0 = xor3(ror32(a, 2), ror32(a, 13), ror32(a, 22));
+    const uint32_t maj = bitop3<0xE8u>(a, b, c);                 // (a & b) ^ (a & c) ^ (b & c)
     const uint32_t t2 = S0 + maj;
     h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
   }
@@ -64,11 +93,11 @@ KHB_HD void sha256_block(uint32_t s[8], uint32_t w[16]) {
 
 // ---- RIPEMD-160 (one block: the 32-byte SHA-256 digest + padding) ----
 KHB_HD uint32_t rmd_f(int j, uint32_t x, uint32_t y, uint32_t z) {
-  return j < 16 ? (x ^ y ^ z)
-       : j < 32 ? ((x & y) | (~x & z))
-       : j < 48 ? ((x | ~y) ^ z)
-       : j < 64 ? ((x & z) | (y & ~z))
-                : (x ^ (y | ~z));
+  return j < 16 ? bitop3<0x96u>(x, y, z)     // x ^ y ^ z
+       : j < 32 ? bitop3<0xCAu>(x, y, z)     // (x & y) | (~x & z)
+       : j < 48 ? bitop3<0x59u>(x, y, z)     // (x | ~y) ^ z
+       : j < 64 ? bitop3<0xE4u>(x, y, z)     // (x & z) | (y & ~z)
+                : bitop3<0x2Du>(x, y, z);    // x ^ (y | ~z)
 }
 
 // digest = SHA-256 state words (big-endian digest bytes); out = RIPEMD-160 state words.

@@ -90,6 +90,10 @@ constexpr bool is_scan(int m) { return m == kScan || is_gated(m); }
 constexpr bool is_addr(int m) { return m >= kAddrU && m <= kAddrDump; }
 constexpr bool needs_y(int m) { return m == kAddrU || m == kAddrB || m == kAddrDump; }
 constexpr bool is_dump(int m) { return m == kDump || m == kAddrDump || m == kBaby || m == kDumpG; }
+#ifndef KHB_ADDR_WAVES_PER_SIMD
+#define KHB_ADDR_WAVES_PER_SIMD KHB_WAVES_PER_SIMD   // occupancy target of the -m address hash kernels
+#endif
+constexpr int waves_per_simd(int m) { return is_addr(m) ? KHB_ADDR_WAVES_PER_SIMD : KHB_WAVES_PER_SIMD; }
 constexpr uint32_t kHalf = KHB_GROUP / 2;            // 512
 constexpr uint32_t kCandCap = 1u << 20;
 constexpr uint32_t kAddrHitCap = 1u << 18;
@@ -1394,7 +1398,7 @@ __device__ __forceinline__ void count_walked(uint32_t* counters, uint32_t walked
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kBlock, KHB_WAVES_PER_SIMD) void k_giant_scan(ScanArgs A) {
+__global__ __launch_bounds__(kBlock, waves_per_simd(MODE)) void k_giant_scan(ScanArgs A) {
   constexpr bool QUEUE = is_scan(MODE);
   constexpr bool BATCH = is_scan(MODE) || MODE == kDump || MODE == kDumpG;
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
