@@ -135,3 +135,6 @@ $(LIBDIR)/variants/libkhbsgs_gs%.so: $(HIP_SRCS) $(DEV_HDRS)
 $(LIBDIR)/variants/aw%/libkhbsgs.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants/aw$*
 	$(HIPCC) $(HIPFLAGS) -DKHB_ADDR_WAVES_PER_SIMD=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/ap%/libkhbsgs.so: $(HIP_SRCS) $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants/ap$*
+	$(HIPCC) $(HIPFLAGS) -DKHB_ADDR_PAIR=1 -DKHB_ADDR_WAVES_PER_SIMD=$* -shared -o $@ $(HIP_SRCS)

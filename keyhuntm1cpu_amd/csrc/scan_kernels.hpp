@@ -93,6 +93,9 @@ constexpr bool is_dump(int m) { return m == kDump || m == kAddrDump || m == kBab
 #ifndef KHB_ADDR_WAVES_PER_SIMD
 #define KHB_ADDR_WAVES_PER_SIMD KHB_WAVES_PER_SIMD   // occupancy target of the -m address hash kernels
 #endif
+#ifndef KHB_ADDR_PAIR
+#define KHB_ADDR_PAIR 0            // -m address 02/03 hashes in one scope (shared SHA-256 schedule words)
+#endif
 constexpr int waves_per_simd(int m) { return is_addr(m) ? KHB_ADDR_WAVES_PER_SIMD : KHB_WAVES_PER_SIMD; }
 constexpr uint32_t kHalf = KHB_GROUP / 2;            // 512
 constexpr uint32_t kCandCap = 1u << 20;
@@ -456,11 +459,18 @@ __device__ __forceinline__ void addr_point(const ScanArgs& A, const Fe& x, const
       }
     };
     if constexpr (MODE == kAddrC || MODE == kAddrB) {
+#if KHB_ADDR_PAIR
+      uint32_t h3[5];
+      hash160_compressed_pair(h, h3, x);
+      if (bloom_check20(A.bloom, A.geom, h)) emit(0);
+      if (bloom_check20(A.bloom, A.geom, h3)) emit(1);
+#else
 #pragma unroll 1
       for (uint32_t pre = 2; pre <= 3; ++pre) {
         hash160_compressed(h, pre, x);
         if (bloom_check20(A.bloom, A.geom, h)) emit(pre - 2);
       }
+#endif
     }
     if constexpr (MODE == kAddrU || MODE == kAddrB) {
       hash160_uncompressed(h, x, y);
