@@ -24,6 +24,10 @@ SHA_BLOCK, RMD_BLOCK, EC_PER_KEY = 2032, 1440, 680
 OPS = {0: 2 * SHA_BLOCK + RMD_BLOCK + EC_PER_KEY,            # uncompressed: 65-byte message, 2 blocks
        1: 2 * (SHA_BLOCK + RMD_BLOCK) + EC_PER_KEY - 150,    # compressed 02 + 03 from x (no y)
        2: 4 * SHA_BLOCK + 3 * RMD_BLOCK + EC_PER_KEY}
+# Executed VALU lane-instructions per key, -l both (rocprofv3 --pmc SQ_INSTS_VALU x 64 / keys of one
+# 8-chunk launch, profiles/r02w/addr_valu_counter_collection.csv: 4.968e12 wave-instr x 64 / 2^35 keys;
+# VALUBusy 101.5 %: the kernel is at the VALU issue ceiling).
+EXEC_PER_KEY = {2: 9253.4}
 PEAK_T = 68.2   # measured v_add_u32 / v_xor issue, 111 lane-ops/clk/CU x 256 CU x 2.4 GHz (profiles/r01_intops2.txt)
 
 
@@ -71,6 +75,13 @@ def main() -> None:
                      "frac_wall": round(OPS[args.search] * rate / 1e12 / PEAK_T, 4),
                      "kernel": "k_giant_scan<address>", "kernel_ms_avg": round(kern * 1e3, 3)},
     }
+    if args.search in EXEC_PER_KEY:
+        e = EXEC_PER_KEY[args.search]
+        out["roofline"]["executed"] = {
+            "valu_lane_instr_per_key": e, "valu_busy_pct": 101.5,
+            "valu_lane_instr_T_per_s_wall": round(e * rate / 1e12, 3),
+            "pmc_source": "profiles/r02w/addr_valu_counter_collection.csv",
+            "note": "fewer executed than algorithmic ops: v_bitop3 / v_alignbit / v_add3 fuse 2-3 simple ops"}
     print(json.dumps(out), flush=True)
 
 
