@@ -138,3 +138,6 @@ $(LIBDIR)/variants/aw%/libkhbsgs.so: $(HIP_SRCS) $(DEV_HDRS)
 $(LIBDIR)/variants/ap%/libkhbsgs.so: $(HIP_SRCS) $(DEV_HDRS)
 	mkdir -p $(LIBDIR)/variants/ap$*
 	$(HIPCC) $(HIPFLAGS) -DKHB_ADDR_PAIR=1 -DKHB_ADDR_WAVES_PER_SIMD=$* -shared -o $@ $(HIP_SRCS)
+$(LIBDIR)/variants/ge%/libkhbsgs.so: $(HIP_SRCS) $(DEV_HDRS)
+	mkdir -p $(LIBDIR)/variants/ge$*
+	$(HIPCC) $(HIPFLAGS) -DKHB_GATE_EARLY=$* -shared -o $@ $(HIP_SRCS)

@@ -295,6 +295,9 @@ struct GatePend {
   __device__ __forceinline__ bool pass() const { return gate_block_pass(lo, hi, bits); }
 };
 
+#ifndef KHB_GATE_EARLY
+#define KHB_GATE_EARLY 0          // 1 = kScanG issues x1's gate load before computing x2 (experiment)
+#endif
 #ifndef KHB_GATE_NT
 #define KHB_GATE_NT 0             // 1 = gate blocks through non-temporal loads (experiment)
 #endif
@@ -331,6 +334,19 @@ __device__ __forceinline__ void gate_pair(const ScanArgs& A, ProbeQueue& Q, cons
     h1 = q1.pass();
     h2 = has2 && q2.pass();
   }
+  if (__ballot(h1 || h2) == 0) return;
+  q_push(Q, h1, x1, job, step1);
+  q_drain(A, Q, kDrainAt);
+  q_push(Q, h2, x2, job, step2);
+  q_drain(A, Q, kDrainAt);
+}
+
+// kScanG with the loads already issued (KHB_GATE_EARLY): x1's block is requested as soon as x1 exists,
+// so its latency hides behind x2's multiply and square.
+__device__ __forceinline__ void gate_pair_pend(const ScanArgs& A, ProbeQueue& Q, const GatePend& q1, const Fe& x1,
+                                               uint32_t step1, const GatePend& q2, const Fe& x2, uint32_t step2,
+                                               uint32_t job) {
+  const bool h1 = q1.pass(), h2 = q2.pass();
   if (__ballot(h1 || h2) == 0) return;
   q_push(Q, h1, x1, job, step1);
   q_drain(A, Q, kDrainAt);
@@ -715,6 +731,18 @@ __device__ __forceinline__ void walk_group_g(const ScanArgs& A, ProbeQueue& Q, c
     fm_mul(s, s, idx);
     fm_sqr_add(x1, s, u);
     x_out<kScanG>(A, x1);
+#if KHB_GATE_EARLY
+    if constexpr (!STAGE1) {
+      const GatePend q1 = gate_issue(A, x1);
+      fm_add_lazy(s, g.y, negCy);             // GSn.y - C.y
+      fm_mul(s, s, idx);
+      fm_sqr_add(x2, s, u);
+      x_out<kScanG>(A, x2);
+      const GatePend q2 = gate_issue(A, x2);
+      gate_pair_pend(A, Q, q1, x1, base + kHalf - 1 - (uint32_t)i, q2, x2, base + kHalf + 1 + (uint32_t)i, job);
+      continue;
+    }
+#endif
     fm_add_lazy(s, g.y, negCy);               // GSn.y - C.y
     fm_mul(s, s, idx);
     fm_sqr_add(x2, s, u);
