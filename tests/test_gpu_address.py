@@ -204,3 +204,19 @@ def test_addr_unsolvedpuzzles_bloom_matches_oracle(eng, ora, search):
     assert len(ref_hits) >= 90
     found, _ = A2.search(base, base + 1024 * 64, search=search, lanes=16384)
     assert sorted(k for k, _, _ in found) == sorted(ref_keys)
+
+
+def test_addr_search_ragged_queue():
+    """The queued device loop (two launches in flight, 8 work items per lane, a short last batch):
+    75 chunks of 2^18 keys at 256 lanes and 4 groups per lane = batches of 32, 32 and 11 chunks, with
+    targets planted in the first, middle and last batches (first and last key of a chunk included);
+    all are found and every key is counted exactly once."""
+    n_seq = 1 << 18
+    lo = 0x1234567 << 18
+    picks = [lo, lo + 40 * n_seq + 777, lo + 74 * n_seq + n_seq - 1, lo + 31 * n_seq + n_seq - 1]
+    text = "\n".join(khhost.hash160(khhost.pubkey(k), True).hex() for k in picks) + "\n"
+    A = khhost.Addr(text, n_seq=n_seq, gpl=4)
+    found, st = A.search(lo, lo + 75 * n_seq, search=1, lanes=256)
+    assert sorted(k for k, _, _ in found) == sorted(picks)
+    assert st["chunks"] == 75 and st["keys"] == 75 * n_seq
+    assert st["launches"] == 3
