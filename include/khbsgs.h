@@ -155,7 +155,8 @@ typedef struct {
 int khb_load_addr_bloom(khb_ctx* ctx, const uint8_t* bf, uint64_t bytes, uint64_t bits, uint32_t hashes);
 /* search: 0 = uncompress, 1 = compress, 2 = both (keyhunt.cpp:59-61, -l).  Every point's hash160(s)
  * are probed in the bloom; bloom hits are returned (the host runs searchbinary and the key
- * recovery).  group_begin must be a multiple of groups_per_lane. */
+ * recovery).  group_begin must be a multiple of groups_per_lane.  Submissions share the context's
+ * two slots with khb_submit (two in flight, FIFO collect, a third returns KHB_EBUSY). */
 int khb_addr_submit(khb_ctx* ctx, const uint8_t* centres_xy_be, uint32_t n_jobs, uint32_t group_begin,
                     uint32_t group_count, int search);
 /* stats->n_cand = number of bloom hits (may exceed cap); giant_steps = keys scanned. */
