@@ -174,6 +174,11 @@ def main():
         workload = "puzzle66 -m bsgs -b 66 -k %d (BASELINE configs[%s])" % (args.k, cfg_idx)
         data = ("real puzzle #66 pubkey (solved key, hash160 == tests/66.rmd), -b 66 range, sequential chunks from "
                 "the chunk after the key's")
+        if lo + world * per_rank * two_n > (1 << 66):
+            # the whole #66 range is 2^20 chunks at k=1 (256 steps of 4096): more ranks x steps than that
+            # continue past 2^66 with the same per-chunk work (no key there, so no early stop)
+            data += ("; the ranks' contiguous blocks continue past 2^66 (the #66 range holds %d steps of this "
+                     "batch after the key's chunk)" % (((1 << 66) - lo) // (args.chunks * two_n)))
         cpu_base = 1 << 65
     else:
         target, line = puzzle130_target()
