@@ -5,10 +5,12 @@
   one step = one GPU scan batch of the product search (libkhhost -> libkhbsgs): host centres for
   4096 chunks, the HIP giant-step kernel over all 4096 groups of each chunk (2^34 giant steps: eight
   8-group work items per lane of a full residency, as the CLI's auto batch), and the CPU confirmation
-  of every candidate, pipelined exactly as the keyhunt_amd CLI runs it.  Chunks are sequential 2N-key
-  chunks of -b 66 starting right after the chunk holding puzzle #66's (public) key, so the search
-  never stops early and every rank times exactly K steps; rank r owns the r-th block of (W + K) x
-  chunks consecutive chunks (weak scaling).
+  of every candidate, pipelined exactly as the keyhunt_amd CLI runs it.  The -b 66 range [2^65, 2^66)
+  is partitioned statically into one contiguous chunk block per rank (partition.key_block, north_star);
+  the block holding puzzle #66's (public) key starts at the chunk after the key's, so the search never
+  stops early and every rank times exactly K steps of sequential 2N-key chunks.  A rank whose W + K
+  steps would run past its block (so past 2^66 for the last rank) is an error: the script exits non-zero
+  before timing (at k=1 and the auto batch each rank's block holds 32 steps at N = 8, 64 at N = 4).
 --workload p130 (BASELINE.json configs[3], -f tests/130.txt -b 130, k=1): the real #130 pubkey; the
   whole -b 130 range [2^129, 2^130) is partitioned statically into one contiguous chunk block per
   rank (partition.rank_range, north_star), and every rank scans (W + K) batches from its block start.
@@ -151,7 +153,7 @@ def main():
             os.close(saved)
 
     from keyhuntm1cpu_amd import khhost
-    from keyhuntm1cpu_amd.partition import rank_range
+    from keyhuntm1cpu_amd.partition import blocks_fit, rank_range
     host_threads = min(16, os.cpu_count() or 1)
     t0 = time.time()
     tables = khhost.Tables(None, args.k, threads=host_threads, gpl=4)
@@ -167,18 +169,20 @@ def main():
     per_rank = (args.warmup + args.steps) * args.chunks
     if args.workload == "p66":
         target = puzzle66_target()
-        key_chunk = (PUZZLE66_KEY - (1 << 65)) // two_n
-        lo = (1 << 65) + (key_chunk + 1) * two_n      # -b 66, after the key's chunk
-        start, end = rank_range(lo, lo + world * per_rank * two_n, two_n, rank, world)
+        lo, hi = 1 << 65, 1 << 66
+        blocks = blocks_fit(lo, hi, two_n, world, per_rank, PUZZLE66_KEY)
+        bad = [r for r, (_, _, ok) in enumerate(blocks) if not ok]
+        if bad:
+            s0, e0, _ = blocks[bad[0]]
+            raise SystemExit("[bench] -b 66 split %d ways: rank %d's block holds %d steps of %d chunks, %d requested "
+                             "(warmup + steps); lower --steps/--warmup/--chunks" %
+                             (world, bad[0], (e0 - s0) // (args.chunks * two_n), args.chunks, args.warmup + args.steps))
+        start, end, _ = blocks[rank]
         cfg_idx = {1: "1", 4: "2"}.get(args.k, "1, k varied")
         workload = "puzzle66 -m bsgs -b 66 -k %d (BASELINE configs[%s])" % (args.k, cfg_idx)
-        data = ("real puzzle #66 pubkey (solved key, hash160 == tests/66.rmd), -b 66 range, sequential chunks from "
-                "the chunk after the key's")
-        if lo + world * per_rank * two_n > (1 << 66):
-            # the whole #66 range is 2^20 chunks at k=1 (256 steps of 4096): more ranks x steps than that
-            # continue past 2^66 with the same per-chunk work (no key there, so no early stop)
-            data += ("; the ranks' contiguous blocks continue past 2^66 (the #66 range holds %d steps of this "
-                     "batch after the key's chunk)" % (((1 << 66) - lo) // (args.chunks * two_n)))
+        data = ("real puzzle #66 pubkey (solved key, hash160 == tests/66.rmd), -b 66 range [2^65, 2^66) split into %d "
+                "static contiguous chunk blocks, one per rank; each rank scans sequential chunks from its block start "
+                "(the key's block from the chunk after the key's); every rank's chunks inside -b 66" % world)
         cpu_base = 1 << 65
     else:
         target, line = puzzle130_target()
@@ -211,32 +215,51 @@ def main():
     dt = time.perf_counter() - t0
     sess.close()
     steps_done = st["giant_steps"]               # counted on the device (khb_collect, count_walked)
+    per_launch_steps = args.chunks * tables.cycles * 1024
     kernel_ms = 1e3 * st["kernel_s"] / max(1, st["launches"])
-    tot_steps, tmax, kmax = steps_done, dt, kernel_ms
+    # device-busy time per step: the union of this rank's launch intervals (HIP events on each launch's
+    # stream, khb_stats.launch_begin_ms/end_ms) over the timed region, per step
+    busy_ms = 1e3 * st["busy_s"] / args.steps
+    bad_count = 0.0 if steps_done == args.steps * per_launch_steps and st["rescans"] == 0 else 1.0
+    tot_steps, tmax, kmax, bmax, bad = steps_done, dt, kernel_ms, busy_ms, bad_count
     if world > 1:
-        v = torch.tensor([float(steps_done), dt, kernel_ms], dtype=torch.float64)
+        v = torch.tensor([float(steps_done), dt, kernel_ms, busy_ms, bad_count], dtype=torch.float64)
         s = v.clone()
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         m = v.clone()
         dist.all_reduce(m, op=dist.ReduceOp.MAX)
-        tot_steps, tmax, kmax = s[0].item(), m[1].item(), m[2].item()
+        tot_steps, tmax, kmax, bmax, bad = s[0].item(), m[1].item(), m[2].item(), m[3].item(), m[4].item()
+    if bad or tot_steps != world * args.steps * per_launch_steps:
+        # a line over an incomplete or repeated count is never printed (every rank exits non-zero)
+        print(f"[bench] ERROR: the device counted {tot_steps:.0f} giant steps over the ranks, "
+              f"{world * args.steps * per_launch_steps} submitted (or a launch was rescanned)", file=sys.stderr, flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        raise SystemExit(3)
 
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
         return
     gsps = tot_steps / tmax
-    per_launch_steps = args.chunks * tables.cycles * 1024
-    if tot_steps != world * args.steps * per_launch_steps:
-        print(f"[bench] WARNING: timed {tot_steps} giant steps, expected {world * args.steps * per_launch_steps}",
+    wall_ms = 1e3 * tmax / args.steps
+    if bmax > wall_ms * 1.0005:
+        print(f"[bench] ERROR: device-busy {bmax:.3f} ms per step exceeds the wall time {wall_ms:.3f} ms",
               file=sys.stderr, flush=True)
-    achieved = OPS_PER_STEP * per_launch_steps / (kernel_ms * 1e-3) / 1e12
-    executed = EXEC_OPS_PER_STEP * per_launch_steps / (kernel_ms * 1e-3) / 1e12
+        raise SystemExit(3)
+    achieved = OPS_PER_STEP * per_launch_steps / (bmax * 1e-3) / 1e12
+    achieved_launch = OPS_PER_STEP * per_launch_steps / (kmax * 1e-3) / 1e12
+    executed = EXEC_OPS_PER_STEP * per_launch_steps / (bmax * 1e-3) / 1e12
     roofline = {"bound": "valu", "unit": "Tops/s", "achieved": round(achieved, 3), "peak": PEAK_MULOPS_T,
                 "frac": round(achieved / PEAK_MULOPS_T, 4), "traffic": None,
                 "ops": "32-bit multiply-class lane ops of the reference algorithm (v_mad_u64_u32 / v_mul_lo_u32)",
                 "ops_per_giant_step": round(OPS_PER_STEP, 2), "kernel": "k_giant_scan",
-                "kernel_ms_avg": round(kernel_ms, 3),
+                "time_basis": "kernel_busy_ms_per_step: union of the k_giant_scan launch intervals over the timed "
+                              "steps (HIP events on each launch's stream) / steps; <= ms_per_step",
+                "kernel_busy_ms_per_step": round(bmax, 3),
+                "kernel_ms_avg": round(kmax, 3),
+                "achieved_per_launch": round(achieved_launch, 3),
+                "frac_per_launch": round(achieved_launch / PEAK_MULOPS_T, 4),
                 "peak_basis": "v_mad_u64_u32 %.1f lane-ops/clk/CU x %d CUs at %.2f GHz (profiles/r01_intops2.txt); "
                               "%.2f T at the 2.4 GHz peak clock" % (PEAK_LANES_PER_CLK_CU, CUS, PEAK_CLK_GHZ,
                                                                     PEAK_MULOPS_T_2P4),
@@ -260,7 +283,7 @@ def main():
                     executed_info.update({
                         "valu_lane_instr_per_giant_step": vi,
                         "valu_busy_pct": pmc.get("valu_busy_pct"),
-                        "valu_lane_instr_T_per_s": round(vi * per_launch_steps / (kernel_ms * 1e-3) / 1e12, 2),
+                        "valu_lane_instr_T_per_s": round(vi * per_launch_steps / (bmax * 1e-3) / 1e12, 2),
                         "vop3_issue_ceiling": "58-61 lane-instr/clk/CU = %.1f-%.1f T at 2.4 GHz (intops2)"
                                               % (58 * CUS * 2.4e-3, 61 * CUS * 2.4e-3),
                         "pmc_source": pmc.get("valu_source")})
@@ -268,10 +291,8 @@ def main():
             pass
     roofline["executed"] = executed_info
     # Two launches overlap (the context's two submission slots): a launch's event time
-    # includes the tail it shares with its neighbour, so the steady-state rate per launch is the
-    # wall time per step.  Both are reported; `achieved` / `frac` keep the per-launch event time
-    # (what rocprofv3's kernel trace shows for k_giant_scan).
-    wall_ms = 1e3 * tmax / args.steps
+    # includes the tail it shares with its neighbour (kernel_ms_avg > ms_per_step), so `achieved` /
+    # `frac` use the device-busy time per step; the per-launch and wall figures are beside them.
     roofline["achieved_wall"] = round(OPS_PER_STEP * per_launch_steps / (wall_ms * 1e-3) / 1e12, 3)
     roofline["frac_wall"] = round(roofline["achieved_wall"] / PEAK_MULOPS_T, 4)
     cpu = None

@@ -57,10 +57,15 @@ typedef struct {
 } khb_degenerate;
 
 typedef struct {
-  uint32_t n_cand;         /* total hits (may exceed the capacity given to khb_collect) */
+  uint32_t n_cand;         /* total hits (may exceed the capacity given to khb_collect, and the ring's
+                              capacity khb_candidate_capacity(): then only that many were kept, and the
+                              caller rescans the submission in parts -- SURVEY.md §8b) */
   uint32_t n_degenerate;
   uint64_t giant_steps;    /* giant steps the device walked (counted on the device: groups x 1024) */
-  float kernel_ms;         /* device time of the scan kernel (HIP events on the ctx stream) */
+  float kernel_ms;         /* device time of the scan kernel (HIP events on the submission's stream) */
+  double launch_begin_ms;  /* the launch's begin and end on the context's clock: ms since the last
+                              khb_reset_epoch (or khb_open); -1 if unavailable.  Two submissions in flight */
+  double launch_end_ms;    /* overlap, so the union of these intervals is the device-busy time. */
 } khb_stats;
 
 /* ---- device / context ---- */
@@ -81,6 +86,17 @@ uint32_t khb_default_lanes(int device);
  * consecutive groups of one job with two field inversions in total, so a launch fills the device
  * when n_jobs * ceil(group_count / khb_groups_per_item()) >= khb_lanes(ctx). */
 uint32_t khb_groups_per_item(void);
+/* Allocate the device state of the first `depth` submission slots now (1 or 2; the second slot's
+ * prefix scratch is ~35 GB on MI355X) instead of on the first queued submission.  KHB_ENOMEM leaves the
+ * extra slot empty and the context usable with one submission in flight (the caller's queue depth 1). */
+int khb_reserve_slots(khb_ctx* ctx, int depth);
+/* Candidate ring entries a -m bsgs launch keeps (default and maximum 2^20).  Lowering it is for tests
+ * of the caller's overflow path (stats.n_cand > capacity -> rescan in parts). */
+int khb_set_candidate_capacity(khb_ctx* ctx, uint32_t cap);
+uint32_t khb_candidate_capacity(const khb_ctx* ctx);
+/* Restart the context's clock (khb_stats.launch_begin_ms / launch_end_ms); KHB_EBUSY while a
+ * submission is in flight. */
+int khb_reset_epoch(khb_ctx* ctx);
 
 /* ---- tables (bsgs setup, keyhunt.cpp:1185-1364) ---- */
 /* Level-1 bloom: 256 sub-blooms of identical geometry concatenated in sub-bloom order
@@ -115,14 +131,18 @@ int khb_load_lane_offsets(khb_ctx* ctx, const uint8_t* offs_xy_be, uint32_t n, u
 /* Enqueue the group loop for n_jobs jobs.  centres[k] (x||y BE) is startP of job k, i.e.
  * target + (order - base - (2M*512 + M))*G (keyhunt.cpp:3861-3869), the centre of group 0.
  * Every job scans groups [group_begin, group_begin + group_count); group_begin must be a
- * multiple of groups_per_lane.  Returns immediately (stream-ordered). */
+ * multiple of groups_per_lane.  Returns immediately (stream-ordered).  A context has two submission
+ * slots, each on its own stream: two submissions may be in flight (their launches overlap), a third
+ * returns KHB_EBUSY until khb_collect retires one. */
 int khb_submit(khb_ctx* ctx, const uint8_t* centres_xy_be, uint32_t n_jobs, uint32_t group_begin,
                uint32_t group_count);
-/* Wait for the last submission; copy up to cap candidates (unordered) and degenerate-group
- * records.  stats may be NULL. */
+/* Wait for the OLDEST submission in flight (FIFO) and retire it; copy up to cap of its candidates
+ * (unordered) and degenerate-group records.  stats may be NULL.  KHB_EINCOMPLETE: the device's count of
+ * walked groups differs from the submission. */
 int khb_collect(khb_ctx* ctx, khb_cand* cand, uint32_t cap, khb_degenerate* degen, uint32_t degen_cap,
                 khb_stats* stats);
-/* Convenience: submit + collect. */
+/* Convenience: submit + collect.  KHB_EBUSY if any submission is in flight (the collect would retire
+ * that one, not this). */
 int khb_scan(khb_ctx* ctx, const uint8_t* centres_xy_be, uint32_t n_jobs, uint32_t group_begin,
              uint32_t group_count, khb_cand* cand, uint32_t cap, khb_stats* stats);
 

@@ -69,7 +69,9 @@ int khh_search(const khh_tables* t, const uint8_t* targets_xy, int n_targets, co
                char* err, size_t errlen);
 
 /* Persistent multi-GPU session: contexts opened and tables resident in HBM once, then any number
- * of searches.  stats_out of khh_session_run: as khh_search plus [5]=scan launches. */
+ * of searches.  stats_out of khh_session_run (8 entries): as khh_search, [6]=launches rescanned in
+ * parts after a candidate-ring overflow, [7]=device-busy microseconds (union of each device's launch
+ * intervals, summed over devices; two launches in flight overlap, so [7] <= [4]). */
 typedef struct khh_session khh_session;
 khh_session* khh_session_open(const khh_tables* t, const int* devices, int n_devices, uint32_t lanes,
                               uint32_t chunks_per_batch, int check_threads, char* err, size_t errlen);
@@ -77,6 +79,14 @@ int khh_session_run(khh_session* s, const uint8_t* targets_xy, int n_targets, co
                     const uint8_t end_be[32], uint64_t max_chunks, int random_chunks, int* found, uint8_t* keys_be,
                     uint64_t* stats_out, char* err, size_t errlen);
 void khh_session_close(khh_session* s);
+/* Test hooks: candidate ring capacity per launch (0 = default 2^20; small values drive the
+ * split-and-rescan path), the level-0 gate on/off, recording of every level-1 candidate of the next
+ * runs (khh_session_recorded), and optionally a replacement level-1 bloom of the tables' geometry
+ * (256 sub-blooms concatenated; NULL keeps the tables'). */
+int khh_session_set_test_hooks(khh_session* s, uint32_t cand_cap, int use_gate, int record, const uint8_t* l1_concat);
+/* Candidates recorded in the last run: chunk base (32 B BE), target index, giant step a; returns the
+ * count (may exceed cap). */
+uint64_t khh_session_recorded(const khh_session* s, uint8_t* bases_be, uint32_t* targets, uint32_t* a, uint64_t cap);
 
 /* helpers */
 int khh_pubkey(const uint8_t key_be[32], uint8_t out_xy[64]);

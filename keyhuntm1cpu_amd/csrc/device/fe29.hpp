@@ -131,9 +131,99 @@ KHB_HD void f9_normalize(F9& r, const uint64_t* c, uint64_t extra, uint32_t k256
   r.v[2] += (uint32_t)(t1 >> 29) + e10 * 256u;          // < 2^13 + 2^19: limb 2 < 2^29 + 2^20
 }
 
+// ---- product and square: high columns first, carried by their high words; low columns seeded ----
+// Column k of a*b is c_k = sum a_i b_(k-i).  With limb bounds A, B (A * B < 2^60.8) a column of up to
+// nine products stays below 2^64.  The reduction uses 2^261 == 2^37 + 31264 (mod p): a value at limb
+// 9 + m equals itself * 31264 at limb m plus * 256 at limb m + 1.
+//  1. high columns k = 9..16, each seeded with 8 * hi32 of the previous one (hi32 of column k sits at
+//     limb k + 1, times 2^3): only the low words lo_k = lo32(c'_k) remain, plus h17 = hi32(c'_16);
+//  2. low columns j = 0..8 in order, each seeded with the carry (t >> 29) of the previous one and
+//     folding lo_(9+j) * 31264 and lo_(8+j) * 256 (and h17 * 8 * 31264 into column 8) in the same
+//     v_mad_u64_u32 chain: no 64-bit additions, one shift and one mask per limb;
+//  3. the value at limb 9, t9 = (t >> 29) + h17 * 8 * 256 (< 2^41), folded into limbs 0..2.
+// Every partial product, seed and fold is one v_mad_u64_u32 (multipliers that are powers of two come
+// from SGPRs, f9_k, so they stay mads).  Output: limbs < 2^29, limb 2 < 2^29 + 2^21 ("strict").
+KHB_HD void f9_final(F9& r, uint64_t t9, uint32_t k256) {
+  const uint32_t e9 = (uint32_t)t9 & KHB_M29, e10 = (uint32_t)(t9 >> 29);      // e10 < 2^12
+  uint64_t t0 = r.v[0];
+  f9_mad(t0, e9, 31264u);                                                   // < 2^45
+  uint64_t t1 = (uint64_t)(r.v[1] + (uint32_t)(t0 >> 29));                  // < 2^29 + 2^16
+  f9_mad(t1, e9, k256);
+  f9_mad(t1, e10, 31264u);                                                  // < 2^38
+  r.v[0] = (uint32_t)t0 & KHB_M29;
+  r.v[1] = (uint32_t)t1 & KHB_M29;
+  r.v[2] += (uint32_t)(t1 >> 29) + e10 * 256u;                              // < 2^9 + 2^20
+}
+
+KHB_HD void f9_mul(F9& r, const F9& a_, const F9& b_) {
+  const F9 a = a_, b = b_;            // r may alias a or b (limbs are written as the low columns complete)
+  const uint32_t k8 = f9_k(8u), k256 = f9_k(256u), k2048 = f9_k(2048u);
+  uint32_t lo[8], hi = 0;
+#pragma unroll
+  for (int k = 9; k < 17; ++k) {
+    f9_fence();
+    uint64_t s = 0;
+    if (k > 9) s = (uint64_t)hi * k8;
+#pragma unroll
+    for (int i = k - 8; i <= 8; ++i) s += (uint64_t)a.v[i] * b.v[k - i];
+    lo[k - 9] = (uint32_t)s;
+    hi = (uint32_t)(s >> 32);
+  }
+  uint64_t t = 0;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    f9_fence();
+    uint64_t s = j ? (t >> 29) : 0;
+#pragma unroll
+    for (int i = 0; i <= j; ++i) s += (uint64_t)a.v[i] * b.v[j - i];
+    if (j < 8) s += (uint64_t)lo[j] * 31264u;
+    if (j > 0) s += (uint64_t)lo[j - 1] * k256;
+    if (j == 8) s += (uint64_t)hi * 250112u;                                  // h17 * 8 * 31264
+    r.v[j] = (uint32_t)s & KHB_M29;
+    t = s;
+  }
+  f9_final(r, (t >> 29) + (uint64_t)hi * k2048, k256);                       // + h17 * 8 * 256
+}
+
+// a^2: 45 products (cross terms against the doubled operand), the same columns and reduction.
+KHB_HD void f9_sqr(F9& r, const F9& a_) {
+  const F9 a = a_;                    // r may alias a
+  const uint32_t k8 = f9_k(8u), k256 = f9_k(256u), k2048 = f9_k(2048u);
+  uint32_t d[9];
+#pragma unroll
+  for (int i = 1; i < 9; ++i) d[i] = a.v[i] << 1;
+  uint32_t lo[8], hi = 0;
+#pragma unroll
+  for (int k = 9; k < 17; ++k) {
+    f9_fence();
+    uint64_t s = 0;
+    if (k > 9) s = (uint64_t)hi * k8;
+    if (!(k & 1)) s += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
+#pragma unroll
+    for (int i = k - 8; 2 * i < k; ++i) s += (uint64_t)a.v[i] * d[k - i];
+    lo[k - 9] = (uint32_t)s;
+    hi = (uint32_t)(s >> 32);
+  }
+  uint64_t t = 0;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    f9_fence();
+    uint64_t s = j ? (t >> 29) : 0;
+    if (!(j & 1)) s += (uint64_t)a.v[j >> 1] * a.v[j >> 1];
+#pragma unroll
+    for (int i = 0; 2 * i < j; ++i) s += (uint64_t)a.v[i] * d[j - i];
+    if (j < 8) s += (uint64_t)lo[j] * 31264u;
+    if (j > 0) s += (uint64_t)lo[j - 1] * k256;
+    if (j == 8) s += (uint64_t)hi * 250112u;
+    r.v[j] = (uint32_t)s & KHB_M29;
+    t = s;
+  }
+  f9_final(r, (t >> 29) + (uint64_t)hi * k2048, k256);
+}
+
 // r = a * b (mod p), strict limbs.  The low columns are accumulated first and each high column
 // is folded as soon as it is complete, so at most one high column is live (register pressure).
-KHB_HD void f9_mul(F9& r, const F9& a, const F9& b) {
+KHB_HD void f9_mul_v1(F9& r, const F9& a, const F9& b) {
   const uint32_t k256 = f9_k(256u), k2048 = f9_k(2048u);
   uint64_t c[9], extra = 0;
 #pragma unroll
@@ -157,7 +247,7 @@ KHB_HD void f9_mul(F9& r, const F9& a, const F9& b) {
 
 // r = a^2 (mod p): cross products against the doubled operand, 45 products; high columns folded
 // as they complete (f9_mul).
-KHB_HD void f9_sqr(F9& r, const F9& a) {
+KHB_HD void f9_sqr_v1(F9& r, const F9& a) {
   const uint32_t k256 = f9_k(256u), k2048 = f9_k(2048u);
   uint32_t d[9];
 #pragma unroll

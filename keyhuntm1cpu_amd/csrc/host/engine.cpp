@@ -63,7 +63,55 @@ struct Batch {
   std::vector<U256> bases;        // chunk bases, in claim order
   std::vector<uint32_t> job_chunk, job_target;
   std::vector<uint8_t> centres;   // 64 B per job
+  uint32_t group_begin = 0;       // groups [group_begin, group_begin + group_count) of every job;
+  uint32_t group_count = 0;       // 0 = the whole chunk
+  bool part = false;              // a rescan part of a batch whose candidate ring overflowed
 };
+
+// The two halves of a batch whose candidates overflowed the ring (the caller rescans):
+// by jobs, or a single job by its group range, cut at a multiple of gpl (khb_submit's alignment).
+// false: a single job of at most gpl groups (cannot be split further).
+bool split_batch(const Batch& b, uint32_t cycles, uint32_t gpl, Batch& lo, Batch& hi) {
+  const size_t nj = b.job_chunk.size();
+  const uint32_t g0 = b.group_begin, gc = b.group_count ? b.group_count : cycles;
+  auto part = [&](Batch& o, size_t j0, size_t j1, uint32_t pb, uint32_t pc) {
+    o.bases = b.bases;
+    o.job_chunk.assign(b.job_chunk.begin() + j0, b.job_chunk.begin() + j1);
+    o.job_target.assign(b.job_target.begin() + j0, b.job_target.begin() + j1);
+    o.centres.assign(b.centres.begin() + 64 * j0, b.centres.begin() + 64 * j1);
+    o.group_begin = pb;
+    o.group_count = pc;
+    o.part = true;
+  };
+  if (nj > 1) {
+    part(lo, 0, nj / 2, g0, gc);
+    part(hi, nj / 2, nj, g0, gc);
+    return true;
+  }
+  if (nj == 0 || gc <= gpl) return false;
+  const uint32_t half = (gc / 2 + gpl - 1) / gpl * gpl;     // gpl <= half < gc
+  part(lo, 0, 1, g0, half);
+  part(hi, 0, 1, g0 + half, gc - half);
+  return true;
+}
+
+// Length of the union of [begin, end) intervals (ms).
+double union_ms(std::vector<std::pair<double, double>>& iv) {
+  std::sort(iv.begin(), iv.end());
+  double tot = 0, b = 0, e = -1;
+  for (const auto& x : iv) {
+    if (x.first < 0 || x.second < x.first) continue;
+    if (x.first > e) {
+      if (e > b) tot += e - b;
+      b = x.first;
+      e = x.second;
+    } else if (x.second > e) {
+      e = x.second;
+    }
+  }
+  if (e > b) tot += e - b;
+  return tot;
+}
 
 bool claim(Shared& S, uint32_t want, Batch& b) {
   std::lock_guard<std::mutex> lk(S.mu);
@@ -186,7 +234,8 @@ uint32_t batch_chunks(const Tables& T, const SearchConfig& cfg, size_t ntargets,
 // One device: up to `queue_depth` batches queued on the GPU (khb_submit fills the context's next
 // slot, each on its own stream, so a queued batch takes over the CUs the running one's last waves
 // free); the next batch is claimed and centred while the GPU scans, and each collected batch is
-// confirmed after its successor has been submitted.
+// confirmed after its successor has been submitted.  A batch whose candidates overflowed the ring
+// is rescanned in two parts (split_batch, recursively), queued ahead of new chunks.
 void device_thread(Shared& S, khb_ctx* ctx) {
   auto fail = [&](int rc, const char* what) {
     std::lock_guard<std::mutex> lk(S.mu);
@@ -196,41 +245,69 @@ void device_thread(Shared& S, khb_ctx* ctx) {
     }
     S.stop = true;
   };
+  auto warn = [&](const std::string& m) {
+    std::lock_guard<std::mutex> lk(S.mu);
+    if (S.cb.on_warning) S.cb.on_warning(m);
+  };
   const Tables& T = S.T;
   const uint32_t cycles = (uint32_t)T.geo.cycles;
   const uint32_t want = batch_chunks(T, S.cfg, S.targets.size(), khb_lanes(ctx));
   const int threads = S.cfg.check_threads > 0 ? S.cfg.check_threads
                                                : (int)std::max(2u, std::min(16u, std::thread::hardware_concurrency()));
-  const int depth = std::max(1, std::min(S.cfg.queue_depth, 2));
+  int depth = std::max(1, std::min(S.cfg.queue_depth, 2));
+  if (depth > 1) {
+    // the second slot's scratch (~35 GB) up front; without it the device runs one batch at a time
+    const int rrc = khb_reserve_slots(ctx, depth);
+    if (rrc == KHB_ENOMEM) {
+      depth = 1;
+      warn("[W] no device memory for a second submission slot: one batch in flight");
+    } else if (rrc) {
+      fail(rrc, "khb_reserve_slots");
+      return;
+    }
+  }
   std::vector<khb_cand> cbuf(1u << 20);
   std::vector<khb_degenerate> dbuf(4096);
+  const uint32_t cap = std::min<uint32_t>(khb_candidate_capacity(ctx), (uint32_t)cbuf.size());
   std::vector<Batch> ring(depth + 1);
-  int next = 0;
+  std::deque<Batch> parts;    // rescan parts of overflowed batches, submitted before new chunks
+  std::vector<std::pair<double, double>> busy;
+  int next = 0;               // ring slots are used and released in FIFO order
   auto take = [&]() { const int i = next; next = (next + 1) % (int)ring.size(); return i; };
   auto stopped = [&]() { std::lock_guard<std::mutex> lk(S.mu); return S.stop; };
   auto prepare = [&](Batch& b) {
-    if (stopped() || !claim(S, want, b)) return false;
+    if (stopped()) return false;
+    if (!parts.empty()) {
+      b = std::move(parts.front());
+      parts.pop_front();
+      return true;
+    }
+    if (!claim(S, want, b)) return false;
+    b.group_begin = b.group_count = 0;
+    b.part = false;
     make_jobs(S, b, threads);
     return !b.job_chunk.empty();
   };
   auto submit = [&](Batch& b) {
-    return khb_submit(ctx, b.centres.data(), (uint32_t)b.job_chunk.size(), 0, cycles);
+    return khb_submit(ctx, b.centres.data(), (uint32_t)b.job_chunk.size(), b.group_begin,
+                      b.group_count ? b.group_count : cycles);
   };
+  int rc = khb_reset_epoch(ctx);
+  if (rc) { fail(rc, "khb_reset_epoch"); return; }
   std::deque<int> q;          // batches on the GPU, oldest first
-  int rc = 0;
-  while ((int)q.size() < depth) {
-    const int i = take();
-    if (!prepare(ring[i])) break;
-    if ((rc = submit(ring[i]))) { fail(rc, "khb_submit"); break; }
-    q.push_back(i);
-  }
+  auto fill = [&]() {         // queue up to `depth` batches (start, and after a rescan drained the queue)
+    while (!rc && (int)q.size() < depth) {
+      if (!prepare(ring[next])) break;
+      const int i = take();
+      if ((rc = submit(ring[i]))) { fail(rc, "khb_submit"); break; }
+      q.push_back(i);
+    }
+  };
+  fill();
   int pre = -1;               // claimed and centred, not yet submitted
   std::vector<khb_cand> cands;
   while (!q.empty()) {
-    if (pre < 0 && !rc) {
-      const int k = take();
-      if (prepare(ring[k])) pre = k;                           // overlaps the GPU scan
-    }
+    if (pre < 0 && !rc && prepare(ring[next])) pre = take();   // overlaps the GPU scan
     const int i = q.front();
     q.pop_front();
     khb_stats st{};
@@ -242,30 +319,49 @@ void device_thread(Shared& S, khb_ctx* ctx) {
     }
     pre = -1;
     if (rc) continue;
-    if (st.n_cand > cbuf.size()) {
-      fail(KHB_ENOMEM, "candidate buffer overflow (lower the batch size)");
-      rc = KHB_ENOMEM;
-      continue;
-    }
     const Batch& b = ring[i];
+    busy.emplace_back(st.launch_begin_ms, st.launch_end_ms);
+    const bool overflow = st.n_cand > cap;
+    if (overflow) {
+      Batch lo, hi;
+      if (!split_batch(b, cycles, T.gpl, lo, hi)) {
+        fail(KHB_ENOMEM, "candidate ring overflow on a single work item");
+        rc = KHB_ENOMEM;
+        continue;
+      }
+      parts.push_front(std::move(hi));
+      parts.push_front(std::move(lo));
+    }
     {
       std::lock_guard<std::mutex> lk(S.mu);
       S.stats.launches += 1;
-      S.stats.chunks += b.bases.size();
-      S.stats.giant_steps += st.giant_steps;
-      S.stats.candidates += st.n_cand;
-      S.stats.degenerate += st.n_degenerate;
       S.stats.kernel_seconds += st.kernel_ms * 1e-3;
-      for (uint32_t d = 0; d < st.n_degenerate && d < dbuf.size(); ++d) {
-        if (!S.cb.on_warning) break;
-        const uint32_t job = dbuf[d].job;
-        S.cb.on_warning("[W] collapsed batch inverse (target on a window centre): chunk 0x" +
-                        b.bases[b.job_chunk[job]].hex() + " group " + std::to_string(dbuf[d].group & 0x7fffffffu));
+      if (!b.part) S.stats.chunks += b.bases.size();
+      if (overflow) {
+        S.stats.rescans += 1;
+      } else {
+        S.stats.giant_steps += st.giant_steps;
+        S.stats.candidates += st.n_cand;
+        S.stats.degenerate += st.n_degenerate;
+        for (uint32_t d = 0; d < st.n_degenerate && d < dbuf.size(); ++d) {
+          if (!S.cb.on_warning) break;
+          const uint32_t job = dbuf[d].job;
+          S.cb.on_warning("[W] collapsed batch inverse (target on a window centre): chunk 0x" +
+                          b.bases[b.job_chunk[job]].hex() + " group " + std::to_string(dbuf[d].group & 0x7fffffffu));
+        }
+        if (S.cfg.record_candidates && S.cb.on_candidate)
+          for (uint32_t c = 0; c < st.n_cand; ++c)
+            S.cb.on_candidate(b.bases[b.job_chunk[cbuf[c].job]], (int)b.job_target[cbuf[c].job], cbuf[c].a);
       }
     }
-    cands.assign(cbuf.begin(), cbuf.begin() + st.n_cand);
-    confirm(S, b, cands, threads);                             // overlaps the GPU scan of the queue
+    if (!overflow) {
+      cands.assign(cbuf.begin(), cbuf.begin() + st.n_cand);
+      confirm(S, b, cands, threads);                           // overlaps the GPU scan of the queue
+    }
+    if (q.empty()) fill();     // rescan parts left after the last batch
   }
+  std::lock_guard<std::mutex> lk(S.mu);
+  S.stats.busy_seconds += union_ms(busy) * 1e-3;
 }
 
 }  // namespace
@@ -284,6 +380,7 @@ int Session::open(const Tables& T, const SearchConfig& cfg, std::string& err) {
     if (!rc && T.gate_log2 && cfg.use_gate) rc = khb_load_gate(c, T.gate.data(), T.gate_log2, T.gate_probes);
     if (!rc) rc = khb_load_giant_table(c, gsn.data());
     if (!rc) rc = khb_load_lane_offsets(c, offs.data(), (uint32_t)T.lane_offs.size(), T.gpl);
+    if (!rc && cfg.cand_cap) rc = khb_set_candidate_capacity(c, cfg.cand_cap);
     if (rc) {
       err = "[E] GPU " + std::to_string(d) + ": " + khb_strerror(rc);
       if (c) khb_close(c);
@@ -292,6 +389,21 @@ int Session::open(const Tables& T, const SearchConfig& cfg, std::string& err) {
     }
     ctx_.push_back(c);
   }
+  return 0;
+}
+
+int Session::set_test_hooks(uint32_t cand_cap, bool use_gate, const uint8_t* l1_concat) {
+  if (!T_) return KHB_ESTATE;
+  for (void* c : ctx_) {
+    khb_ctx* x = (khb_ctx*)c;
+    int rc = khb_set_candidate_capacity(x, cand_cap ? cand_cap : (1u << 20));
+    if (!rc && l1_concat) rc = khb_load_bloom(x, l1_concat, T_->l1[0].bytes, T_->l1[0].bits, T_->l1[0].hashes);
+    if (!rc) rc = use_gate && T_->gate_log2 ? khb_load_gate(x, T_->gate.data(), T_->gate_log2, T_->gate_probes)
+                                            : khb_load_gate(x, nullptr, 0, 0);
+    if (rc) return rc;
+  }
+  cfg_.cand_cap = cand_cap;
+  cfg_.use_gate = use_gate;
   return 0;
 }
 

@@ -35,6 +35,9 @@ struct SearchConfig {
   bool random_chunks = false;      // -B random: every chunk base drawn uniformly in the range
   bool use_gate = true;            // load the tables' level-0 gate (khb_load_gate) when they have one
   int queue_depth = 2;             // batches queued per device (1 or 2; 2 overlaps launch tails)
+  uint32_t cand_cap = 0;           // candidate ring entries per launch (0 = library default, 2^20); tests
+                                   // lower it to drive the overflow path (split + rescan)
+  bool record_candidates = false;  // tests: report every level-1 candidate (SearchCallbacks::on_candidate)
 };
 
 struct SearchStats {
@@ -43,7 +46,10 @@ struct SearchStats {
   uint64_t giant_steps = 0;
   uint64_t candidates = 0;
   uint64_t degenerate = 0;
-  double kernel_seconds = 0;       // summed over devices
+  uint64_t rescans = 0;            // launches whose candidate ring overflowed and were rescanned in parts
+  double kernel_seconds = 0;       // summed over launches and devices (per-launch event time)
+  double busy_seconds = 0;         // union of each device's launch intervals, summed over devices: the
+                                   // device-busy time (two launches in flight overlap, so < kernel_seconds)
 };
 
 struct SearchCallbacks {
@@ -52,6 +58,9 @@ struct SearchCallbacks {
   // progress: base of the chunk a device just claimed (for `-q`-less "Thread 0x..." lines)
   std::function<void(const U256& base)> on_chunk;
   std::function<void(const std::string& msg)> on_warning;
+  // every level-1 candidate (chunk base, target, giant step a) of a complete launch, before its check
+  // (only with SearchConfig::record_candidates)
+  std::function<void(const U256& base, int k, uint32_t a)> on_candidate;
 };
 
 // A set of opened devices with the tables resident in HBM (libkhbsgs contexts), reusable across
@@ -68,6 +77,10 @@ class Session {
           uint64_t max_chunks = 0, bool random_chunks = false);
   void close();
   const SearchConfig& config() const { return cfg_; }
+  SearchConfig& config() { return cfg_; }
+  // tests: candidate ring capacity per launch (0 = default), the level-0 gate on/off, and optionally
+  // a replacement level-1 bloom of the same geometry (256 sub-blooms concatenated; null = the tables')
+  int set_test_hooks(uint32_t cand_cap, bool use_gate, const uint8_t* l1_concat = nullptr);
 
  private:
   const Tables* T_ = nullptr;

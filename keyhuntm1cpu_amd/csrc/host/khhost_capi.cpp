@@ -171,6 +171,12 @@ int khh_secondcheck(const khh_tables* t, const uint8_t base_be[32], uint32_t a, 
 
 struct khh_session {
   Session s;
+  bool record = false;                 // tests: keep every level-1 candidate of the last run
+  struct Rec {
+    U256 base;
+    uint32_t target, a;
+  };
+  std::vector<Rec> recorded;
 };
 
 khh_session* khh_session_open(const khh_tables* t, const int* devices, int n_devices, uint32_t lanes,
@@ -200,6 +206,9 @@ int khh_session_run(khh_session* s, const uint8_t* targets_xy, int n_targets, co
   std::vector<Target> tg((size_t)n_targets);
   for (int k = 0; k < n_targets; ++k) tg[k].p = pt_from_be(targets_xy + 64 * k);
   SearchCallbacks cb;
+  s->recorded.clear();
+  if (s->record)
+    cb.on_candidate = [s](const U256& base, int k, uint32_t a) { s->recorded.push_back({base, (uint32_t)k, a}); };
   std::vector<int> f;
   std::vector<U256> keys;
   SearchStats st;
@@ -217,9 +226,28 @@ int khh_session_run(khh_session* s, const uint8_t* targets_xy, int n_targets, co
     stats_out[3] = st.degenerate;
     stats_out[4] = (uint64_t)(st.kernel_seconds * 1e6);
     stats_out[5] = st.launches;
+    stats_out[6] = st.rescans;
+    stats_out[7] = (uint64_t)(st.busy_seconds * 1e6);
   }
   if (rc) set_err(err, errlen, e);
   return rc;
+}
+
+int khh_session_set_test_hooks(khh_session* s, uint32_t cand_cap, int use_gate, int record, const uint8_t* l1_concat) {
+  if (!s) return KHB_EINVAL;
+  s->s.config().record_candidates = record != 0;
+  s->record = record != 0;
+  return s->s.set_test_hooks(cand_cap, use_gate != 0, l1_concat);
+}
+
+uint64_t khh_session_recorded(const khh_session* s, uint8_t* bases_be, uint32_t* targets, uint32_t* a, uint64_t cap) {
+  if (!s) return 0;
+  for (uint64_t i = 0; i < s->recorded.size() && i < cap; ++i) {
+    if (bases_be) s->recorded[i].base.to_be(bases_be + 32 * i);
+    if (targets) targets[i] = s->recorded[i].target;
+    if (a) a[i] = s->recorded[i].a;
+  }
+  return s->recorded.size();
 }
 
 int khh_search(const khh_tables* t, const uint8_t* targets_xy, int n_targets, const uint8_t start_be[32],
@@ -228,8 +256,10 @@ int khh_search(const khh_tables* t, const uint8_t* targets_xy, int n_targets, co
                char* err, size_t errlen) {
   khh_session* s = khh_session_open(t, devices, n_devices, lanes, chunks_per_batch, 0, err, errlen);
   if (!s) return KHB_ENODEV;
-  int rc = khh_session_run(s, targets_xy, n_targets, start_be, end_be, max_chunks, 0, found, keys_be, stats_out,
-                           err, errlen);
+  uint64_t st8[8] = {0};
+  int rc = khh_session_run(s, targets_xy, n_targets, start_be, end_be, max_chunks, 0, found, keys_be, st8, err,
+                           errlen);
+  if (stats_out) memcpy(stats_out, st8, 6 * sizeof(uint64_t));   // khh_search's stats hold 6
   khh_session_close(s);
   return rc;
 }

@@ -113,7 +113,7 @@ struct Slot {
   uint32_t* d_ahits = nullptr;         // -m address hits
   uint32_t* d_counters = nullptr;
   uint32_t* h_counters = nullptr;      // pinned
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;   // launch begin / end (khb_stats: kernel_ms, launch_*_ms)
   uint64_t pending_steps = 0;
   int kind = 0;                        // in flight: 1 = -m bsgs scan, 2 = -m address scan
 };
@@ -139,6 +139,8 @@ struct khb_ctx {
   Slot slot[kQueueDepth];              // slot[0] also serves the synchronous helpers (dump, self-tests)
   int head = 0;                        // oldest in-flight slot
   int queued = 0;                      // submissions in flight (0..kQueueDepth)
+  uint32_t cand_cap = kCandCap;        // candidate ring entries a launch may fill (khb_set_candidate_capacity)
+  hipEvent_t epoch = nullptr;          // time origin of khb_stats.launch_begin_ms / launch_end_ms (khb_reset_epoch)
   // -m address
   uint8_t* d_abloom = nullptr;
   BloomGeom ageom{};
@@ -169,10 +171,12 @@ uint64_t walked_groups(const Slot& S) {
 // Entries (32 B) of lane-private scratch: scan_group needs 512, scan_batch kBatch*514 + kBatch.
 constexpr size_t kScratchEntries = (size_t)kBatch * (kHalf + 3) > kHalf ? (size_t)kBatch * (kHalf + 3) : kHalf;
 
-// Device state of a slot, created on its first use (a context that never queues a second
-// submission never pays for a second scratch).
-int ensure_slot(khb_ctx* c, Slot& S) {
-  if (S.d_scratch) return KHB_OK;
+void free_slot(Slot& S);
+
+// Device state of a slot: slot 0 at khb_open, slot 1 on the first queued submission or up front by
+// khb_reserve_slots.  A failure part-way frees what was allocated, so the slot is either complete or
+// empty (and the caller may go on with the slots it has).
+int ensure_slot_alloc(khb_ctx* c, Slot& S) {
   KHB_TRY(c, hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
   KHB_TRY(c, hipMalloc(&S.d_scratch, (KHB_F9WALK ? sizeof(F9) : sizeof(Fe)) * kScratchEntries * c->lanes));
   KHB_TRY(c, hipMalloc(&S.d_cand, sizeof(khb_cand) * kCandCap));
@@ -182,6 +186,13 @@ int ensure_slot(khb_ctx* c, Slot& S) {
   KHB_TRY(c, hipEventCreate(&S.ev0));
   KHB_TRY(c, hipEventCreate(&S.ev1));
   return KHB_OK;
+}
+
+int ensure_slot(khb_ctx* c, Slot& S) {
+  if (S.ev1) return KHB_OK;            // complete (ev1 is created last)
+  const int rc = ensure_slot_alloc(c, S);
+  if (rc) free_slot(S);
+  return rc;
 }
 
 void free_slot(Slot& S) {
@@ -250,9 +261,24 @@ ScanArgs make_args(khb_ctx* c, const Slot& S, uint32_t n_jobs, uint32_t group_be
   A.lanes_per_job = (group_count + per_item - 1) / per_item;
   A.n_items = (uint64_t)n_jobs * A.lanes_per_job;
   A.stride = c->lanes;
-  A.cand_cap = kCandCap;
+  A.cand_cap = c->cand_cap;
   A.degen_cap = kDegenCap;
   return A;
+}
+
+// kernel_ms and the launch's interval on the context's clock (khb_reset_epoch), from the slot's events.
+void launch_times(const khb_ctx* c, const Slot& S, khb_stats* st) {
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, S.ev0, S.ev1) != hipSuccess) ms = -1.f;
+  st->kernel_ms = ms;
+  float b = -1.f, e = -1.f;
+  if (c->epoch && hipEventElapsedTime(&b, c->epoch, S.ev0) == hipSuccess &&
+      hipEventElapsedTime(&e, c->epoch, S.ev1) == hipSuccess) {
+    st->launch_begin_ms = b;
+    st->launch_end_ms = e;
+  } else {
+    st->launch_begin_ms = st->launch_end_ms = -1.0;
+  }
 }
 
 int check_scan_args(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count,
@@ -305,6 +331,34 @@ void* khb_stream(khb_ctx* c) { return c ? (void*)c->slot[0].stream : nullptr; }
 uint32_t khb_lanes(const khb_ctx* c) { return c ? c->lanes : 0; }
 uint32_t khb_groups_per_item(void) { return kBatch; }
 
+int khb_reserve_slots(khb_ctx* c, int depth) {
+  if (!c || depth < 1 || depth > kQueueDepth) return KHB_EINVAL;
+  if (c->queued) return KHB_EBUSY;
+  KHB_TRY(c, hipSetDevice(c->device));
+  for (int i = 1; i < depth; ++i) {
+    const int rc = ensure_slot(c, c->slot[i]);
+    if (rc) return rc;                 // the slot is left empty (ensure_slot frees a partial one)
+  }
+  return KHB_OK;
+}
+
+int khb_set_candidate_capacity(khb_ctx* c, uint32_t cap) {
+  if (!c || cap == 0 || cap > kCandCap) return KHB_EINVAL;
+  if (c->queued) return KHB_EBUSY;
+  c->cand_cap = cap;
+  return KHB_OK;
+}
+
+uint32_t khb_candidate_capacity(const khb_ctx* c) { return c ? c->cand_cap : 0; }
+
+int khb_reset_epoch(khb_ctx* c) {
+  if (!c) return KHB_EINVAL;
+  if (c->queued) return KHB_EBUSY;
+  KHB_TRY(c, hipSetDevice(c->device));
+  KHB_TRY(c, hipEventRecord(c->epoch, c->slot[0].stream));
+  return KHB_OK;
+}
+
 uint32_t khb_default_lanes(int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return 0;
@@ -338,6 +392,8 @@ int khb_open(int device, uint32_t lanes, khb_ctx** out) {
   c->lanes = lanes;
   hipError_t e = hipSetDevice(device);
   int rc = e == hipSuccess ? ensure_slot(c, c->slot[0]) : hip_fail(c, e);
+  if (!rc && (e = hipEventCreate(&c->epoch)) == hipSuccess) e = hipEventRecord(c->epoch, c->slot[0].stream);
+  if (!rc && e != hipSuccess) rc = hip_fail(c, e);
   if (rc) {
     khb_close(c);
     return rc;
@@ -350,6 +406,7 @@ int khb_close(khb_ctx* c) {
   if (!c) return KHB_OK;
   if (c->device >= 0) hipSetDevice(c->device);
   for (Slot& S : c->slot) free_slot(S);
+  if (c->epoch) hipEventDestroy(c->epoch);
   hipFree(c->d_bloom);
   hipFree(c->d_gate);
   hipFree(c->d_gate1);
@@ -494,7 +551,7 @@ int khb_collect(khb_ctx* c, khb_cand* cand, uint32_t cap, khb_degenerate* degen,
   c->queued--;
   KHB_TRY(c, hipStreamSynchronize(S.stream));
   const uint32_t nc = S.h_counters[0], nd = S.h_counters[1];
-  uint32_t take = nc < kCandCap ? nc : kCandCap;
+  uint32_t take = nc < c->cand_cap ? nc : c->cand_cap;
   if (take > cap) take = cap;
   if (take && cand) KHB_TRY(c, hipMemcpy(cand, S.d_cand, sizeof(khb_cand) * take, hipMemcpyDeviceToHost));
   uint32_t dt = nd < kDegenCap ? nd : kDegenCap;
@@ -505,15 +562,14 @@ int khb_collect(khb_ctx* c, khb_cand* cand, uint32_t cap, khb_degenerate* degen,
     st->n_cand = nc;
     st->n_degenerate = nd;
     st->giant_steps = steps;
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, S.ev0, S.ev1) != hipSuccess) ms = -1.f;
-    st->kernel_ms = ms;
+    launch_times(c, S, st);
   }
   return steps == S.pending_steps ? KHB_OK : KHB_EINCOMPLETE;
 }
 
 int khb_scan(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count,
              khb_cand* cand, uint32_t cap, khb_stats* st) {
+  if (c && c->queued) return KHB_EBUSY;   // khb_collect would retire the older submission, not this one
   int rc = khb_submit(c, centres, n_jobs, group_begin, group_count);
   if (rc) return rc;
   return khb_collect(c, cand, cap, nullptr, 0, st);
@@ -669,15 +725,14 @@ int khb_addr_collect(khb_ctx* c, khb_addr_hit* hits, uint32_t cap, khb_stats* st
     st->n_cand = nh;
     st->n_degenerate = nd;
     st->giant_steps = steps;
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, S.ev0, S.ev1) != hipSuccess) ms = -1.f;
-    st->kernel_ms = ms;
+    launch_times(c, S, st);
   }
   return steps == S.pending_steps ? KHB_OK : KHB_EINCOMPLETE;
 }
 
 int khb_addr_scan(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count,
                   int search, khb_addr_hit* hits, uint32_t cap, khb_stats* st) {
+  if (c && c->queued) return KHB_EBUSY;   // as khb_scan
   int rc = khb_addr_submit(c, centres, n_jobs, group_begin, group_count, search);
   if (rc) return rc;
   return khb_addr_collect(c, hits, cap, st);

@@ -33,7 +33,7 @@ class AddrHit(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("n_cand", C.c_uint32), ("n_degenerate", C.c_uint32), ("giant_steps", C.c_uint64),
-                ("kernel_ms", C.c_float)]
+                ("kernel_ms", C.c_float), ("launch_begin_ms", C.c_double), ("launch_end_ms", C.c_double)]
 
 
 _libs: dict[str, C.CDLL] = {}
@@ -61,6 +61,13 @@ def lib(path: str | None = None) -> C.CDLL:
         L.khb_default_lanes.argtypes = [C.c_int]
         L.khb_groups_per_item.restype = C.c_uint32
         L.khb_groups_per_item.argtypes = []
+        for name in ("khb_reserve_slots", "khb_set_candidate_capacity"):
+            if hasattr(L, name):                 # absent only in older timing builds
+                getattr(L, name).argtypes = [C.c_void_p, C.c_uint32 if "capacity" in name else C.c_int]
+        if hasattr(L, "khb_candidate_capacity"):
+            L.khb_candidate_capacity.restype = C.c_uint32
+            L.khb_candidate_capacity.argtypes = [C.c_void_p]
+            L.khb_reset_epoch.argtypes = [C.c_void_p]
         L.khb_load_bloom.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, C.c_uint64, C.c_uint32]
         L.khb_load_giant_table.argtypes = [C.c_void_p, C.c_char_p]
         L.khb_load_gate.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32]
@@ -135,6 +142,18 @@ class Engine:
 
     def stream(self) -> int:
         return int(self.L.khb_stream(self.h) or 0)
+
+    def reserve_slots(self, depth: int) -> None:
+        _check(self.L.khb_reserve_slots(self.h, depth), self.h, self.L)
+
+    def set_candidate_capacity(self, cap: int) -> None:
+        _check(self.L.khb_set_candidate_capacity(self.h, cap), self.h, self.L)
+
+    def candidate_capacity(self) -> int:
+        return int(self.L.khb_candidate_capacity(self.h))
+
+    def reset_epoch(self) -> None:
+        _check(self.L.khb_reset_epoch(self.h), self.h, self.L)
 
     def load_bloom(self, bf: bytes, bytes_per_sub: int, bits: int, hashes: int) -> None:
         assert len(bf) == 256 * bytes_per_sub

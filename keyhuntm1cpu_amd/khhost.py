@@ -58,6 +58,9 @@ def lib() -> C.CDLL:
         L.khh_session_run.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, C.c_uint64, C.c_int,
                                       P(C.c_int), C.c_char_p, P(C.c_uint64), C.c_char_p, C.c_size_t]
         L.khh_session_close.argtypes = [C.c_void_p]
+        L.khh_session_set_test_hooks.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_char_p]
+        L.khh_session_recorded.restype = C.c_uint64
+        L.khh_session_recorded.argtypes = [C.c_void_p, C.c_char_p, P(C.c_uint32), P(C.c_uint32), C.c_uint64]
         L.khh_pubkey.argtypes = [C.c_char_p, C.c_char_p]
         L.khh_parse_pubkey.argtypes = [C.c_char_p, C.c_char_p, P(C.c_int)]
         L.khh_addr_new.restype = C.c_void_p
@@ -223,7 +226,7 @@ class Tables:
                      "kernel_s": stats[4] / 1e6, "launches": stats[5]}
 
 
-_STAT_KEYS = ("chunks", "giant_steps", "candidates", "degenerate", "kernel_s", "launches")
+_STAT_KEYS = ("chunks", "giant_steps", "candidates", "degenerate", "kernel_s", "launches", "rescans", "busy_s")
 
 
 class Session:
@@ -253,7 +256,7 @@ class Session:
         n = len(targets_xy)
         found = (C.c_int * n)()
         keys = C.create_string_buffer(32 * n)
-        stats = (C.c_uint64 * 6)()
+        stats = (C.c_uint64 * 8)()
         err = C.create_string_buffer(256)
         rc = lib().khh_session_run(self.h, b"".join(targets_xy), n, _b32(start), _b32(end), max_chunks,
                                    1 if random_chunks else 0, found, keys, stats, err, 256)
@@ -262,7 +265,24 @@ class Session:
         res = [int.from_bytes(keys.raw[32 * i:32 * i + 32], "big") if found[i] else None for i in range(n)]
         st = {k: int(stats[i]) for i, k in enumerate(_STAT_KEYS)}
         st["kernel_s"] = stats[4] / 1e6
+        st["busy_s"] = stats[7] / 1e6
         return res, st
+
+    def set_test_hooks(self, cand_cap: int = 0, use_gate: bool = True, record: bool = False,
+                       l1_concat: bytes | None = None) -> None:
+        """Tests: candidate ring capacity (0 = default), gate on/off, candidate recording, replacement L1."""
+        rc = lib().khh_session_set_test_hooks(self.h, cand_cap, 1 if use_gate else 0, 1 if record else 0, l1_concat)
+        if rc:
+            raise KhhError(f"set_test_hooks failed ({rc})")
+
+    def recorded(self) -> list[tuple[int, int, int]]:
+        """Level-1 candidates of the last run: (chunk base, target index, a)."""
+        n = lib().khh_session_recorded(self.h, None, None, None, 0)
+        bases = C.create_string_buffer(32 * max(1, n))
+        tg = (C.c_uint32 * max(1, n))()
+        a = (C.c_uint32 * max(1, n))()
+        lib().khh_session_recorded(self.h, bases, tg, a, n)
+        return [(int.from_bytes(bases.raw[32 * i:32 * i + 32], "big"), int(tg[i]), int(a[i])) for i in range(n)]
 
 
 # ---- -m address / -m rmd160 ----

@@ -19,3 +19,21 @@ def rank_range(lo: int, hi: int, two_n: int, rank: int, world: int) -> tuple[int
     start = min(hi, lo + first * two_n)
     end = min(hi, start + count * two_n)
     return start, end
+
+
+def key_block(lo: int, hi: int, two_n: int, rank: int, world: int, key: int | None = None) -> tuple[int, int]:
+    """rank_range, except that the block holding `key` starts at the chunk after the key's chunk (chunks
+    counted from lo): a timed scan of a solved puzzle's range then never stops early on its key."""
+    start, end = rank_range(lo, hi, two_n, rank, world)
+    if key is not None and start <= key < end:
+        start = min(end, lo + ((key - lo) // two_n + 1) * two_n)
+    return start, end
+
+
+def blocks_fit(lo: int, hi: int, two_n: int, world: int, chunks_per_rank: int, key: int | None = None):
+    """Every rank's (start, end, fits): fits = the rank's chunks_per_rank chunks end inside its block."""
+    out = []
+    for r in range(world):
+        s, e = key_block(lo, hi, two_n, r, world, key)
+        out.append((s, e, s + chunks_per_rank * two_n <= e))
+    return out

@@ -117,3 +117,37 @@ def test_two_queued_submissions_fifo(ora):
             assert sorted(a for jj, a in cands if jj == j) == sorted(ref)
     assert [a for jj, a in got[0][0] if jj == 0]         # the key's chunk (batch 0, chunk 0) has a hit
     t.close()
+
+
+def test_scan_refused_while_submission_pending():
+    """khb_scan (submit + collect) with a submission in flight returns KHB_EBUSY instead of collecting
+    the older submission's results as its own (the FIFO collect); after the pending one is collected it
+    runs.  The launch intervals of khb_stats lie on the context's clock (khb_reset_epoch) in order."""
+    from keyhuntm1cpu_amd.khbsgs import Engine, KhbError
+    t = khhost.Tables("0x100000000", 1, threads=8)
+    tgt = khhost.pubkey(0x2000000000123457)
+    with Engine(0, lanes=16384) as e:
+        bf, nb, bits, h = t.bloom_concat(1)
+        e.load_bloom(bf, nb, bits, h)
+        e.load_giant_table(t.giant_table())
+        offs, gpl = t.lane_offsets()
+        e.load_lane_offsets(offs, gpl)
+        e.reserve_slots(2)
+        e.reset_epoch()
+        c0 = t.chunk_centre(0x2000000000000000, tgt)
+        c1 = t.chunk_centre(0x2000000200000000, tgt)
+        import ctypes as C
+        from keyhuntm1cpu_amd.khbsgs import Cand, Stats
+        buf, st = (Cand * 4096)(), Stats()
+        e.submit(c0, 0, t.cycles)
+        assert e.L.khb_scan(e.h, c1, 1, 0, t.cycles, buf, 4096, C.byref(st)) == -6      # KHB_EBUSY
+        with pytest.raises(KhbError, match="in flight"):
+            e.reset_epoch()
+        cands0, _, st0 = e.collect()
+        assert [a for _, a in cands0]                      # the key's chunk: its true hit
+        assert e.L.khb_scan(e.h, c1, 1, 0, t.cycles, buf, 4096, C.byref(st)) == 0
+        st1 = st
+        assert st0.giant_steps == st1.giant_steps == t.cycles * 1024
+        assert 0 <= st0.launch_begin_ms < st0.launch_end_ms <= st1.launch_begin_ms < st1.launch_end_ms
+        assert abs((st0.launch_end_ms - st0.launch_begin_ms) - st0.kernel_ms) < 0.05
+    t.close()

@@ -51,3 +51,39 @@ def test_partition_ragged():
         rs = [rank_range(10, 10 + 5 * 64 + 3, 64, r, world) for r in range(world)]
         assert rs[0][0] == 10 and rs[-1][1] == 10 + 5 * 64 + 3
         assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+
+
+P66_KEY = 0x2832ED74F2B5E35EE        # puzzle #66's public solution (tests/66.rmd; bench.PUZZLE66_KEY)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_p66_static_blocks(world):
+    """bench.py --workload p66 for N ranks: -b 66 split into N static blocks (keyhunt.cpp:508-527 sets
+    the -b range, north_star partitions it); the key's block starts at the chunk after the key's; the
+    driver's 5 warmup + 20 timed steps of 4096 chunks (k = 1, 2N = 2^45) fit inside every block."""
+    from keyhuntm1cpu_amd.partition import blocks_fit, key_block
+    chunks = (5 + 20) * 4096
+    blocks = blocks_fit(LO, HI, TWO_N, world, chunks, P66_KEY)
+    assert all(ok for _, _, ok in blocks)
+    for r, (s, e, _) in enumerate(blocks):
+        rs, re_ = rank_range(LO, HI, TWO_N, r, world)
+        assert LO <= rs <= s < s + chunks * TWO_N <= e == re_ <= HI
+        assert (s - LO) % TWO_N == 0
+        if rs <= P66_KEY < re_:
+            assert s == LO + ((P66_KEY - LO) // TWO_N + 1) * TWO_N    # right after the key's chunk
+        else:
+            assert s == rs
+    assert sum(1 for r in range(world) if rank_range(LO, HI, TWO_N, r, world)[0] <= P66_KEY
+               < rank_range(LO, HI, TWO_N, r, world)[1]) == 1
+    if world == 1:   # the single-GPU line's range is unchanged from round 2: from the chunk after the key's
+        assert key_block(LO, HI, TWO_N, 0, 1, P66_KEY)[0] == LO + ((P66_KEY - LO) // TWO_N + 1) * TWO_N
+
+
+def test_p66_blocks_overrun_detected():
+    """bench.py's default 5 + 100 steps fit one GPU (190 steps after the key's chunk) but not a 2-, 4- or
+    8-way split of -b 66 (the key's block then holds 62 / 62 / 30 steps after it): the bench must refuse
+    them rather than scan past the block or 2^66."""
+    from keyhuntm1cpu_amd.partition import blocks_fit
+    for world in (2, 4, 8):
+        assert not all(ok for _, _, ok in blocks_fit(LO, HI, TWO_N, world, 105 * 4096, P66_KEY))
+    assert all(ok for _, _, ok in blocks_fit(LO, HI, TWO_N, 1, 105 * 4096, P66_KEY))
