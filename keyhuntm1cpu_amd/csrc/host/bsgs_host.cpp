@@ -425,9 +425,16 @@ void Tables::chunk_aux_run(const U256& base0, size_t n, Pt* aux, int threads) co
   jd[2] = mul_g(secp_order() - geo.N_double * 2ull);         // not D + D: AddDirect cannot double
   for (size_t j = 3; j < kAuxBlock; ++j) jd[j] = add_direct(jd[j - 1], D);
   const size_t blocks = (n + kAuxBlock - 1) / kAuxBlock;
+  const U256 lim = secp_order() - geo.intaux;                // chunk_aux's km = lim - base wraps at base > lim
   auto body = [&](size_t blk) {
     const size_t s = blk * kAuxBlock, m = std::min(kAuxBlock, n - s);
     const U256 bs = base0 + geo.N_double * (uint64_t)s;
+    if (bs >= lim || lim - bs <= geo.N_double * (uint64_t)(m - 1)) {
+      // the block reaches the group order: km of a later chunk is 0 (the identity) or wraps mod 2^256
+      // (not mod n) in chunk_aux, which the walk from the block start would not reproduce
+      for (size_t j = 0; j < m; ++j) aux[s + j] = chunk_aux(bs + geo.N_double * (uint64_t)j);
+      return;
+    }
     aux[s] = chunk_aux(bs);
     if (m < 2) return;
     std::vector<Pt> a(m - 1, aux[s]);

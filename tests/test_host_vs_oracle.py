@@ -114,6 +114,7 @@ def test_batched_job_centres(ora):
     oracle's chunk start (keyhunt.cpp:3861-3869): consecutive runs crossing block boundaries, a run
     whose first auxiliary point equals 5 * (-2N G) (the doubling fallback), and random bases."""
     import random
+    N_ORDER = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
     t = khhost.Tables("0x1000000", 1, threads=4)
     o = ora.Bsgs("0x1000000", 1, 4)
     two_n = 2 * t.n_low
@@ -122,7 +123,10 @@ def test_batched_job_centres(ora):
     rng = random.Random(7)
     runs = [[(1 << 40) + c * two_n for c in range(200)],
             [5 * two_n - intaux + c * two_n for c in range(70)],
-            [rng.randrange(1, 1 << 250) for _ in range(40)]]
+            [rng.randrange(1, 1 << 250) for _ in range(40)],
+            # runs reaching the group order: km = n - base - intaux hits 0 and then wraps (advisor r2)
+            [N_ORDER - intaux - 37 * two_n + c * two_n for c in range(70)],
+            [N_ORDER - intaux - 3 * two_n + 5 + c * two_n for c in range(8)]]
     for bases in runs:
         got = t.job_centres(bases, tg)
         assert got == b"".join(t.chunk_centre(b, x) for b in bases for x in tg)
