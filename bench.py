@@ -14,6 +14,11 @@
 --workload p130 (BASELINE.json configs[3], -f tests/130.txt -b 130, k=1): the real #130 pubkey; the
   whole -b 130 range [2^129, 2^130) is partitioned statically into one contiguous chunk block per
   rank (partition.rank_range, north_star), and every rank scans (W + K) batches from its block start.
+--workload address (BASELINE.json configs[4], -m address -f tests/unsolvedpuzzles.rmd, -l both): one step =
+  8 chunks of 2^32 keys (one queued launch of ~8 work items per lane) through the product address search
+  (SHA-256 + RIPEMD-160 kernels, bloom hits confirmed on the host); -b 71's range [2^70, 2^71) split
+  into static rank blocks.  The line's metric is keys hashed and probed per second; use a small --steps
+  (a step is ~8 s at -l both).
 
 Tables are built and resident in HBM before the timed region.  Multi-GPU: one process per GPU
 (torch.distributed.run); no data-path collective (gloo only times it).
@@ -110,8 +115,10 @@ def cpu_baseline(seconds: float, threads: int, target, base: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", choices=("p66", "p130"), default="p66",
-                    help="p66: BASELINE configs[1] (-b 66; --k 4 = configs[2]); p130: configs[3] (-b 130)")
+    ap.add_argument("--workload", choices=("p66", "p130", "address"), default="p66",
+                    help="p66: BASELINE configs[1] (-b 66; --k 4 = configs[2]); p130: configs[3] (-b 130); "
+                         "address: configs[4] (-m address unsolvedpuzzles.rmd, -l both)")
+    ap.add_argument("--search", type=int, default=2, help="--workload address: -l 0 uncompress, 1 compress, 2 both")
     # default: >= 30 s of steady state — 100 steps x 2^34 giant steps at ~360 ms
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
@@ -155,6 +162,8 @@ def main():
     from keyhuntm1cpu_amd import khhost
     from keyhuntm1cpu_amd.partition import blocks_fit, rank_range
     host_threads = min(16, os.cpu_count() or 1)
+    if args.workload == "address":
+        return bench_address(args, world, rank, dist, torch)
     t0 = time.time()
     tables = khhost.Tables(None, args.k, threads=host_threads, gpl=4)
     t_build = time.time() - t0
@@ -257,6 +266,7 @@ def main():
                 "time_basis": "kernel_busy_ms_per_step: union of the k_giant_scan launch intervals over the timed "
                               "steps (HIP events on each launch's stream) / steps; <= ms_per_step",
                 "kernel_busy_ms_per_step": round(bmax, 3),
+                "shader_mhz_avg": round(st["shader_mhz"], 1),
                 "kernel_ms_avg": round(kmax, 3),
                 "achieved_per_launch": round(achieved_launch, 3),
                 "frac_per_launch": round(achieved_launch / PEAK_MULOPS_T, 4),
@@ -335,6 +345,136 @@ def main():
     if world > 1:
         dist.destroy_process_group()
 
+
+
+# -m address (configs[4]).  Executed VALU lane-instructions per key at -l both: PMC SQ_INSTS_VALU x 64 / keys
+# of one 8-chunk launch (profiles/r02w/addr_valu_counter_collection.csv, 4.968e12 x 64 / 2^35).  The
+# issue ceiling is that of the kernel's own instruction mix: the hash blocks are 43 % full-rate VALU
+# (v_add_u32, v_bitop3_b32, shifts: ~2.6 SIMD cycles per wave-instruction at 4 waves/SIMD) and 57 %
+# half-rate (v_alignbit_b32, v_add3_u32, v_mad_u64_u32: ~4.6), profiles/r03_valu_cost.txt and
+# tools/debug/bb_path.py over tools/microbench/hash_isa.hip = 3.73 cycles per wave-instruction.
+ADDR_EXEC_VALU_PER_KEY = {2: 9253.4}
+ADDR_MIX_CYCLES_PER_INSTR = 3.73
+ADDR_ALG_OPS = {0: 2 * 2032 + 1440 + 680, 1: 2 * (2032 + 1440) + 530, 2: 4 * 2032 + 3 * 1440 + 680}
+
+
+def addr_cpu_baseline(text: str, seconds: float, threads: int, search: int):
+    """Oracle restatement of thread_process's group loop (ora_addr.c) on `threads` host threads."""
+    import threading
+    from oracle import ora
+    A = ora.AddrTable(text)
+    done = [0] * threads
+    stop = time.perf_counter() + seconds
+
+    def work(t):
+        g = ora.AddrGen(1)
+        key = (1 << 70) + t * (1 << 40)
+        while time.perf_counter() < stop:
+            g.group(A, key, search)
+            key += 1024
+            done[t] += 1024
+        g.close()
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    el = time.perf_counter() - t0
+    A.close()
+    return sum(done) / el
+
+
+def bench_address(args, world, rank, dist, torch):
+    from keyhuntm1cpu_amd import khhost
+    from keyhuntm1cpu_amd.partition import rank_range
+    n_seq, chunks = 1 << 32, args.chunks or 8
+    with open(os.path.join(REPO, "tests", "golden", "address", "unsolvedpuzzles.rmd")) as f:
+        text = f.read()
+    t0 = time.time()
+    A = khhost.Addr(text, n_seq=n_seq, threads=min(16, os.cpu_count() or 1))
+    t_build = time.time() - t0
+    lo, hi = 1 << 70, 1 << 71
+    start, end = rank_range(lo, hi, n_seq, rank, world)
+    per_rank = (args.warmup + args.steps) * chunks
+    if start + per_rank * n_seq > end:
+        raise SystemExit("[bench] -b 71 block too small for the requested steps")
+    if args.warmup:
+        A.search(start, start + args.warmup * chunks * n_seq, search=args.search)
+    tstart = start + args.warmup * chunks * n_seq
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    found, st = A.search(tstart, tstart + args.steps * chunks * n_seq, search=args.search)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    keys = st["keys"]
+    bad = 0.0 if keys == args.steps * chunks * n_seq else 1.0
+    tot, tmax, mhz = float(keys), dt, st["shader_mhz"]
+    if world > 1:
+        v = torch.tensor([float(keys), dt, bad, mhz], dtype=torch.float64)
+        s, m = v.clone(), v.clone()
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        tot, tmax, bad, mhz = s[0].item(), m[1].item(), m[2].item(), s[3].item() / world
+    if bad:
+        print(f"[bench] ERROR: the device counted {tot:.0f} keys, {world * args.steps * chunks * n_seq} submitted",
+              file=sys.stderr, flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        raise SystemExit(3)
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    rate = tot / tmax
+    per_gpu = rate / world
+    roofline = {"bound": "valu", "unit": "T lane-instr/s", "kernel": "k_giant_scan<address>",
+                "time_basis": "wall time of the timed steps (two launches in flight, as the CLI runs them)",
+                "shader_mhz_avg": round(mhz, 1)}
+    e = ADDR_EXEC_VALU_PER_KEY.get(args.search)
+    if e and mhz > 0:
+        peak = CUS * 4 * 64 / ADDR_MIX_CYCLES_PER_INSTR * mhz * 1e6 / 1e12
+        ach = e * per_gpu / 1e12
+        roofline.update({"achieved": round(ach, 3), "peak": round(peak, 3), "frac": round(ach / peak, 4),
+                         "valu_lane_instr_per_key": e,
+                         "peak_basis": "the hash mix's issue ceiling, %.2f SIMD cycles per wave-instruction (43 %% "
+                                       "full-rate / 57 %% half-rate VALU, profiles/r03_valu_cost.txt) x 1024 SIMDs at "
+                                       "the launches' measured shader clock" % ADDR_MIX_CYCLES_PER_INSTR,
+                         "executed_source": "profiles/r02w/addr_valu_counter_collection.csv (PMC SQ_INSTS_VALU)"})
+    roofline["algorithmic_ops_per_key"] = ADDR_ALG_OPS[args.search]
+    roofline["traffic"] = None
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        c_threads, hinfo = host_cores()
+        v = addr_cpu_baseline(text, args.cpu_seconds, c_threads, args.search)
+        cpu = {"value": round(v / 1e6, 4), "unit": "Mkeys/s", "cores": c_threads, "kind": "port",
+               "sample": f"oracle ora_addr_group (thread_process group loop restatement, -l "
+                         f"{['uncompress', 'compress', 'both'][args.search]}), keys from 2^70, {args.cpu_seconds:.0f} s "
+                         f"on {c_threads} threads", "host": hinfo}
+    out = {
+        "metric": "Mkeys/s (-m address: keys hashed and bloom-probed per second) on 1/2/4/8 MI355X",
+        "value": round(rate / 1e6, 2), "unit": "Mkeys/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * tmax / args.steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "real target file tests/unsolvedpuzzles.rmd (the reference's, committed as a fixture), -b 71 range "
+                "[2^70, 2^71) split into static rank blocks, sequential 2^32-key chunks",
+        "config": {"workload": "-m address -f tests/unsolvedpuzzles.rmd -l %s -b 71 (BASELINE configs[4])"
+                               % ["uncompress", "compress", "both"][args.search],
+                   "targets": len(A.table()), "n_seq": hex(n_seq), "chunks_per_step": chunks,
+                   "keys_per_step": chunks * n_seq, "parallelism": "range-partition x%d" % world,
+                   "table_build_s": round(t_build, 2), "bloom_hits": st["hits"], "found": len(found),
+                   "launches": st["launches"]},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    A.close()
+    if world > 1:
+        dist.destroy_process_group()
 
 if __name__ == "__main__":
     main()

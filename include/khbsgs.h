@@ -66,6 +66,8 @@ typedef struct {
   double launch_begin_ms;  /* the launch's begin and end on the context's clock: ms since the last
                               khb_reset_epoch (or khb_open); -1 if unavailable.  Two submissions in flight */
   double launch_end_ms;    /* overlap, so the union of these intervals is the device-busy time. */
+  float shader_mhz;        /* average shader clock over the launch (s_memtime / s_memrealtime of its first
+                              wave), 0 if unavailable */
 } khb_stats;
 
 /* ---- device / context ---- */

@@ -69,9 +69,10 @@ int khh_search(const khh_tables* t, const uint8_t* targets_xy, int n_targets, co
                char* err, size_t errlen);
 
 /* Persistent multi-GPU session: contexts opened and tables resident in HBM once, then any number
- * of searches.  stats_out of khh_session_run (8 entries): as khh_search, [6]=launches rescanned in
+ * of searches.  stats_out of khh_session_run (9 entries): as khh_search, [6]=launches rescanned in
  * parts after a candidate-ring overflow, [7]=device-busy microseconds (union of each device's launch
- * intervals, summed over devices; two launches in flight overlap, so [7] <= [4]). */
+ * intervals, summed over devices; two launches in flight overlap, so [7] <= [4]), [8]=average shader clock
+ * of the launches in kHz (9 entries in all). */
 typedef struct khh_session khh_session;
 khh_session* khh_session_open(const khh_tables* t, const int* devices, int n_devices, uint32_t lanes,
                               uint32_t chunks_per_batch, int check_threads, char* err, size_t errlen);
@@ -106,8 +107,8 @@ void khh_addr_giant_table(const khh_addr* a, uint8_t out[513 * 64]);
 uint32_t khh_addr_lane_offsets(const khh_addr* a, uint8_t* out /* n*64, may be NULL */, uint32_t* gpl);
 /* Sequential (random_chunks = 0) or -R search of [start, end) with search 0/1/2 (-l).  Found keys
  * (32 B BE each) with compressed flags and rmd160s, in discovery order; *n_found may exceed cap.
- * stats_out (nullable, 6): [0]=chunks [1]=keys [2]=bloom hits [3]=degenerate groups [4]=kernel us
- * [5]=launches. */
+ * stats_out (nullable, 7): [0]=chunks [1]=keys [2]=bloom hits [3]=degenerate groups [4]=kernel us
+ * [5]=launches [6]=average shader clock of the launches in kHz. */
 int khh_addr_search(const khh_addr* a, const uint8_t start_be[32], const uint8_t end_be[32], int search,
                     int random_chunks, const int* devices, int n_devices, uint32_t lanes, uint64_t max_chunks,
                     uint8_t* keys_be, uint8_t* compressed, uint8_t* rmd, uint32_t cap, uint32_t* n_found,

@@ -78,59 +78,6 @@ KHB_HD void f9_fence() {
 #endif
 }
 
-// t >> 29.  KHB_F9_SHR = 1: one v_lshrrev_b64; 2: v_alignbit_b32 for the low word and a 32-bit shift
-// for the high word.
-#ifndef KHB_F9_SHR
-#define KHB_F9_SHR 1
-#endif
-KHB_HD uint64_t f9_shr29(uint64_t t) {
-#if defined(__HIP_DEVICE_COMPILE__) && KHB_F9_SHR == 2
-  const uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32);
-  return ((uint64_t)(hi >> 29) << 32) | __builtin_amdgcn_alignbit(hi, lo, 29);
-#else
-  return t >> 29;
-#endif
-}
-
-// Fold the high column k = 9 + j (value h, < 2^64) into the low columns c[0..8] (and the value
-// left at limb 9, extra): h's lo word sits at limb k, its hi word at limb k (weight
-// 2^(29k + 32)) = 8 * hi at limb k + 1, and 2^261 == 2^37 + 31264 moves limb 9 + j to limbs j, j + 1.
-KHB_HD void f9_fold_col(uint64_t* c, uint64_t& extra, int j, uint64_t h, uint32_t k256, uint32_t k2048) {
-  const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
-  f9_mad(c[j], lo, 31264u);                             // < 2^47
-  f9_mad(c[j + 1], lo, k256);                           // < 2^40
-  f9_mad(c[j + 1], hi, 250112u);                        // 8 * 31264: < 2^50
-  if (j + 2 <= 8)
-    f9_mad(c[j + 2], hi, k2048);                        // 8 * 256: < 2^43
-  else
-    extra = (uint64_t)hi * k2048;                       // j = 7: hi of column 16 (< 2^29)
-}
-
-// Normalise the folded low columns c[0..8] (each < 2^64) into strict limbs.
-KHB_HD void f9_normalize(F9& r, const uint64_t* c, uint64_t extra, uint32_t k256) {
-  // t ends as the value at limb 9 (< 2^36)
-  uint64_t t = c[0];
-  r.v[0] = (uint32_t)t & KHB_M29;
-  t = f9_shr29(t);
-#pragma unroll
-  for (int i = 1; i < 9; ++i) {
-    t += c[i];
-    r.v[i] = (uint32_t)t & KHB_M29;
-    t = f9_shr29(t);
-  }
-  // fold the value at limb 9 (< 2^40) as two limbs: e9 (29 bits) at limb 9 and e10 at limb 10
-  t += extra;
-  const uint32_t e9 = (uint32_t)t & KHB_M29, e10 = (uint32_t)(t >> 29);
-  uint64_t t0 = r.v[0];
-  f9_mad(t0, e9, 31264u);                               // < 2^45
-  uint64_t t1 = r.v[1] + (t0 >> 29);
-  f9_mad(t1, e9, k256);
-  f9_mad(t1, e10, 31264u);                              // < 2^42
-  r.v[0] = (uint32_t)t0 & KHB_M29;
-  r.v[1] = (uint32_t)t1 & KHB_M29;
-  r.v[2] += (uint32_t)(t1 >> 29) + e10 * 256u;          // < 2^13 + 2^19: limb 2 < 2^29 + 2^20
-}
-
 // ---- product and square: high columns first, carried by their high words; low columns seeded ----
 // Column k of a*b is c_k = sum a_i b_(k-i).  With limb bounds A, B (A * B < 2^60.8) a column of up to
 // nine products stays below 2^64.  The reduction uses 2^261 == 2^37 + 31264 (mod p): a value at limb
@@ -219,54 +166,6 @@ KHB_HD void f9_sqr(F9& r, const F9& a_) {
     t = s;
   }
   f9_final(r, (t >> 29) + (uint64_t)hi * k2048, k256);
-}
-
-// r = a * b (mod p), strict limbs.  The low columns are accumulated first and each high column
-// is folded as soon as it is complete, so at most one high column is live (register pressure).
-KHB_HD void f9_mul_v1(F9& r, const F9& a, const F9& b) {
-  const uint32_t k256 = f9_k(256u), k2048 = f9_k(2048u);
-  uint64_t c[9], extra = 0;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    uint64_t s = (uint64_t)a.v[0] * b.v[k];
-#pragma unroll
-    for (int i = 1; i <= k; ++i) s += (uint64_t)a.v[i] * b.v[k - i];
-    c[k] = s;
-  }
-#pragma unroll
-  for (int k = 9; k < 17; ++k) {
-    f9_fence();
-    uint64_t s = (uint64_t)a.v[k - 8] * b.v[8];
-#pragma unroll
-    for (int i = k - 7; i <= 8; ++i) s += (uint64_t)a.v[i] * b.v[k - i];
-    f9_fold_col(c, extra, k - 9, s, k256, k2048);
-  }
-  f9_fence();
-  f9_normalize(r, c, extra, k256);
-}
-
-// r = a^2 (mod p): cross products against the doubled operand, 45 products; high columns folded
-// as they complete (f9_mul).
-KHB_HD void f9_sqr_v1(F9& r, const F9& a) {
-  const uint32_t k256 = f9_k(256u), k2048 = f9_k(2048u);
-  uint32_t d[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;      // < 2^31.4
-  uint64_t c[9], extra = 0;
-#pragma unroll
-  for (int k = 0; k < 17; ++k) {
-    const int lo = k > 8 ? k - 8 : 0;
-    uint64_t s = (k & 1) ? 0 : (uint64_t)a.v[k >> 1] * a.v[k >> 1];
-#pragma unroll
-    for (int i = lo; 2 * i < k; ++i) s += (uint64_t)a.v[i] * d[k - i];
-    if (k < 9) {
-      c[k] = s;
-    } else {
-      f9_fold_col(c, extra, k - 9, s, k256, k2048);
-      f9_fence();
-    }
-  }
-  f9_normalize(r, c, extra, k256);
 }
 
 KHB_HD void f9_sqr_n(F9& r, const F9& a, int n) {

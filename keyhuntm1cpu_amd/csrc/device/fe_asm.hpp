@@ -26,21 +26,13 @@ namespace khb {
 
 #define FM_DEV __device__ __forceinline__
 
-// KHB_RARE: carry/borrow propagation past limb 1/2 that happens with probability ~2^-30 per call
+// Rare carries: carry/borrow propagation past limb 1/2 that happens with probability ~2^-30 per call
 // (the fold of 2^256 = 0x1000003D1 into a random 256-bit value) runs behind a wave-uniform branch
 // taken only when some lane needs it; the common path stops the chain at the limb that produces
 // the carry.  The branch body is the full propagation, a no-op for lanes whose carry is 0.
-// KHB_NOP: the one wait state between a VCC (carry) write and its VALU reader.  KHB_NONOP=1 drops
-// it: a timing-only build (wrong results) that bounds what the pads cost.
-#if KHB_NONOP
-#define KHB_NOP ""
-#else
+// KHB_NOP: the one wait state between a VCC (carry) write and its VALU reader.  (A timing-only build
+// without it was 1.1 % faster, profiles/r01_nonop_ab.txt; the pads stay as the hazard rule asks.)
 #define KHB_NOP "s_nop 0\n\t"
-#endif
-
-#ifndef KHB_RARE
-#define KHB_RARE 1
-#endif
 #if KHB_RARE_FORCE    // test builds: always take the rare branch (its full propagation is a no-op at c = 0)
 FM_DEV bool fm_any(uint32_t) { return true; }
 #else
@@ -68,29 +60,6 @@ FM_DEV void fm_madc(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
       : "+v"(acc), "+v"(c2)
       : "v"(a), "v"(b)
       : "vcc");
-}
-
-template <int K>
-FM_DEV void fm_col(uint64_t& acc, uint32_t& c2, const uint32_t* a, const uint32_t* b) {
-#pragma unroll
-  for (int i = (K > 7 ? K - 7 : 0); i <= (K < 7 ? K : 7); ++i) fm_madc(acc, c2, a[i], b[K - i]);
-}
-
-// 512-bit product, product scanning (column k = sum of a_i*b_{k-i}).
-FM_DEV void fm_mul512(uint32_t t[16], const uint32_t* a, const uint32_t* b) {
-  uint64_t acc = (uint64_t)a[0] * b[0];
-  t[0] = (uint32_t)acc;
-  acc >>= 32;
-  uint32_t c2 = 0;
-#define FM_COL(K)                                      \
-  fm_col<K>(acc, c2, a, b);                            \
-  t[K] = (uint32_t)acc;                                \
-  acc = (acc >> 32) | ((uint64_t)c2 << 32);            \
-  c2 = 0;
-  FM_COL(1) FM_COL(2) FM_COL(3) FM_COL(4) FM_COL(5) FM_COL(6) FM_COL(7)
-  FM_COL(8) FM_COL(9) FM_COL(10) FM_COL(11) FM_COL(12) FM_COL(13) FM_COL(14)
-#undef FM_COL
-  t[15] = (uint32_t)acc;
 }
 
 // ---- 512-bit products without accumulator shuffling ----------------------------------------
@@ -187,46 +156,6 @@ FM_DEV void fm_mul512x(uint32_t t[16], const uint32_t* a, const uint32_t* b) {
   fm_fold_cols(t, A, cw[13]);
 }
 
-// t_k = lo(cur) + hi(prev); the carry c_k joins cw (the carries of column k-1) as the seed of
-// column k+1, which has the same weight.  seed <= 8, so seeding never overflows a column.
-FM_DEV void fm_fold_step(uint32_t& t, uint32_t& seed, uint64_t cur, uint64_t prev, uint32_t cw) {
-  asm("v_add_co_u32_e32 %0, vcc, %2, %3\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %1, vcc, 0, %4, vcc"
-      : "=&v"(t), "=v"(seed)
-      : "v"((uint32_t)cur), "v"((uint32_t)(prev >> 32)), "v"(cw)
-      : "vcc");
-}
-
-// 512-bit product, seeded columns folded as they complete: only two column accumulators are
-// ever live (the all-columns-then-fold form above needs 15 pairs at its peak).
-FM_DEV void fm_mul512p(uint32_t t[16], const uint32_t* a, const uint32_t* b) {
-  uint32_t cw[14], seed;
-  uint64_t prev = (uint64_t)a[0] * b[0], cur;
-  t[0] = (uint32_t)prev;
-  cur = 0;
-  fm_colx<1>(cur, cw[1], a, b);
-  fm_fold_step(t[1], seed, cur, prev, 0u);
-  prev = cur;
-#define FM_COLP(K)                                 \
-  cur = (uint64_t)seed;                            \
-  fm_colx<K>(cur, cw[K], a, b);                    \
-  fm_fold_step(t[K], seed, cur, prev, cw[K - 1]);  \
-  prev = cur;
-  FM_COLP(2) FM_COLP(3) FM_COLP(4) FM_COLP(5) FM_COLP(6) FM_COLP(7) FM_COLP(8) FM_COLP(9) FM_COLP(10)
-  FM_COLP(11) FM_COLP(12) FM_COLP(13)
-#undef FM_COLP
-  // column 14: one product, no carry; t15 = hi(A14) + cw13 + c14
-  cur = (uint64_t)seed;
-  cur += (uint64_t)a[7] * b[7];
-  asm("v_add_co_u32_e32 %0, vcc, %2, %3\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %1, vcc, %4, %5, vcc"
-      : "=&v"(t[14]), "=v"(t[15])
-      : "v"((uint32_t)cur), "v"((uint32_t)(prev >> 32)), "v"(cw[13]), "v"((uint32_t)(cur >> 32))
-      : "vcc");
-}
-
 // Column K of the cross sum sum_{i<j} a_i a_j 2^(32(i+j)).
 template <int K>
 FM_DEV void fm_colsq(uint64_t& A, uint32_t& cw, const uint32_t* a) {
@@ -237,85 +166,6 @@ FM_DEV void fm_colsq(uint64_t& A, uint32_t& cw, const uint32_t* a) {
 #pragma unroll
     for (int i = lo + 2; i <= hi; ++i) fm_madc(A, cw, a[i], a[K - i]);
   }
-}
-
-// t_k = d_k + 2 c_k, word 1 (starts both carry chains): u = d + c -> carry sU; t = u + c -> sT.
-// The chains run across columns whose products use VCC, so their carries live in SGPR pairs
-// (VOP3 forms).
-FM_DEV void fm_sq_word_first(uint32_t& t, uint64_t& sU, uint64_t& sT, uint32_t d, uint32_t c) {
-  uint32_t u;
-  asm("v_add_co_u32_e64 %0, %2, %4, %5\n\t"
-      "v_add_co_u32_e64 %1, %3, %0, %5"
-      : "=&v"(u), "=v"(t), "=&s"(sU), "=&s"(sT)
-      : "v"(d), "v"(c));
-}
-FM_DEV void fm_sq_word(uint32_t& t, uint64_t& sU, uint64_t& sT, uint32_t d, uint32_t c) {
-  uint32_t u;
-  asm(KHB_NOP
-      "v_addc_co_u32_e64 %0, %2, %4, %5, %2\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e64 %1, %3, %0, %5, %3"
-      : "=&v"(u), "=v"(t), "+s"(sU), "+s"(sT)
-      : "v"(d), "v"(c));
-}
-
-// a^2 progressively: cross-sum words c_k are folded as their columns complete and immediately
-// combined with the diagonal words d_k; peak liveness is the 16 output words plus a handful.
-FM_DEV void fm_sqr512p(uint32_t t[16], const uint32_t* a) {
-  uint32_t cw[14], seed, c;
-  uint64_t prev, cur, sU, sT, D;
-  D = (uint64_t)a[0] * a[0];
-  t[0] = (uint32_t)D;
-  // column 1: a0*a1
-  cur = (uint64_t)a[0] * a[1];
-  c = (uint32_t)cur;
-  seed = 0;
-  fm_sq_word_first(t[1], sU, sT, (uint32_t)(D >> 32), c);
-  prev = cur;
-  // column 2: a0*a2 (single product; the fold of word 2 creates the first seed)
-  cur = (uint64_t)a[0] * a[2];
-  fm_fold_step(c, seed, cur, prev, 0u);
-  D = (uint64_t)a[1] * a[1];
-  fm_sq_word(t[2], sU, sT, (uint32_t)D, c);
-  prev = cur;
-#define FM_SQP(K, CWPREV, DWORD)                   \
-  cur = (uint64_t)seed;                            \
-  fm_colsq<K>(cur, cw[K], a);                      \
-  fm_fold_step(c, seed, cur, prev, CWPREV);        \
-  fm_sq_word(t[K], sU, sT, DWORD, c);              \
-  prev = cur;
-  FM_SQP(3, 0u, (uint32_t)(D >> 32))
-  D = (uint64_t)a[2] * a[2];
-  FM_SQP(4, cw[3], (uint32_t)D)
-  FM_SQP(5, cw[4], (uint32_t)(D >> 32))
-  D = (uint64_t)a[3] * a[3];
-  FM_SQP(6, cw[5], (uint32_t)D)
-  FM_SQP(7, cw[6], (uint32_t)(D >> 32))
-  D = (uint64_t)a[4] * a[4];
-  FM_SQP(8, cw[7], (uint32_t)D)
-  FM_SQP(9, cw[8], (uint32_t)(D >> 32))
-  D = (uint64_t)a[5] * a[5];
-  FM_SQP(10, cw[9], (uint32_t)D)
-  FM_SQP(11, cw[10], (uint32_t)(D >> 32))
-  D = (uint64_t)a[6] * a[6];
-#undef FM_SQP
-  // columns 12, 13: single products (5,7), (6,7): no cw of their own
-  cur = (uint64_t)seed;
-  cur += (uint64_t)a[5] * a[7];
-  fm_fold_step(c, seed, cur, prev, cw[11]);
-  fm_sq_word(t[12], sU, sT, (uint32_t)D, c);
-  prev = cur;
-  cur = (uint64_t)seed;
-  cur += (uint64_t)a[6] * a[7];
-  fm_fold_step(c, seed, cur, prev, 0u);
-  fm_sq_word(t[13], sU, sT, (uint32_t)(D >> 32), c);
-  prev = cur;
-  // column 14 holds no cross product: c14 = seed + hi(A13); c15 = its carry
-  D = (uint64_t)a[7] * a[7];
-  cur = (uint64_t)seed;
-  fm_fold_step(c, seed, cur, prev, 0u);
-  fm_sq_word(t[14], sU, sT, (uint32_t)D, c);
-  fm_sq_word(t[15], sU, sT, (uint32_t)(D >> 32), seed);
 }
 
 // a^2 = 2*cross + diag: 36 products instead of 64.
@@ -563,7 +413,6 @@ FM_DEV void fm_reduce_T(Fe& r, const uint32_t T[10], const uint32_t* H) {
   const uint64_t w = (uint64_t)(uint32_t)(u >> 32) + R8;                              // limb-1 addend
   const uint32_t w2 = (uint32_t)(w >> 32) + R9;                                       // limb-2 addend (<= 3)
   uint32_t c;
-#if KHB_RARE
   // limbs 0..2 take the addends; the carry into limb 3 (probability ~2^-30) is propagated, and
   // a wrap past 2^256 (~2^-212) folded, only in the rare branch.
   uint32_t c3;
@@ -588,102 +437,27 @@ FM_DEV void fm_reduce_T(Fe& r, const uint32_t T[10], const uint32_t* H) {
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) r.v[i] = R[i];
-  return;
-#endif
-  asm("v_add_co_u32_e32 %0, vcc, %0, %9\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %1, vcc, %1, %10, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %2, vcc, %2, %11, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %4, vcc, 0, %4, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %5, vcc, 0, %5, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %7, vcc, 0, %7, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %8, vcc, 0, %12, vcc"
-      : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]), "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]), "=&v"(c)
-      : "v"((uint32_t)u), "v"((uint32_t)w), "v"(w2), "v"(0u)
-      : "vcc");
-  // c = 1 only when R wrapped past 2^256, leaving R < 2^67: add 2^256 mod p = 2^32 + 977 once
-  // more (limbs 0..3 suffice: the sum stays < 2^68).
-  const uint32_t k0 = c * 977u;
-  asm("v_add_co_u32_e32 %0, vcc, %0, %4\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %1, vcc, %1, %5, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %3, vcc, 0, %3, vcc"
-      : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3])
-      : "v"(k0), "v"(c)
-      : "vcc");
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = R[i];
 }
 
-// Production multiply/square: seeded-column schedule (fm_mul512x / fm_sqr512x).
-// Schedules: 0 = column shuffle, 1 = seeded columns folded at the end, 2 = folded as they complete.
-#ifndef KHB_MUL_IMPL
-#define KHB_MUL_IMPL 1
-#endif
-#ifndef KHB_SQR_IMPL
-#define KHB_SQR_IMPL 1
-#endif
+// Multiply / square: seeded columns (fm_mul512x / fm_sqr512x), then the reduction.  (The column-shuffle
+// and fold-as-completed schedules were measured slower: profiles/r01_fmbench.txt.)
 FM_DEV void fm_mul(Fe& r, const Fe& a, const Fe& b) {
   uint32_t t[16];
-#if KHB_MUL_IMPL == 0
-  fm_mul512(t, a.v, b.v);
-#elif KHB_MUL_IMPL == 1
   fm_mul512x(t, a.v, b.v);
-#else
-  fm_mul512p(t, a.v, b.v);
-#endif
   fm_reduce(r, t);
 }
 
 FM_DEV void fm_sqr(Fe& r, const Fe& a) {
   uint32_t t[16];
-#if KHB_SQR_IMPL == 0
-  fm_mul512(t, a.v, a.v);
-#elif KHB_SQR_IMPL == 1
   fm_sqr512x(t, a.v);
-#else
-  fm_sqr512p(t, a.v);
-#endif
   fm_reduce(r, t);
 }
 
 // r = a^2 + w (mod p), lazy; w < 2^256 (fm_reduce_add).
 FM_DEV void fm_sqr_add(Fe& r, const Fe& a, const Fe& w) {
   uint32_t t[16];
-#if KHB_SQR_IMPL == 0
-  fm_mul512(t, a.v, a.v);
-#elif KHB_SQR_IMPL == 1
   fm_sqr512x(t, a.v);
-#else
-  fm_sqr512p(t, a.v);
-#endif
   fm_reduce_add(r, t, w);
-}
-
-// Previous schedule (column shuffle, squaring as a general product), kept as the
-// microbenchmark / exactness baseline (tools/microbench/fmbench.hip).
-FM_DEV void fm_mul_shuffle(Fe& r, const Fe& a, const Fe& b) {
-  uint32_t t[16];
-  fm_mul512(t, a.v, b.v);
-  fm_reduce(r, t);
-}
-
-FM_DEV void fm_sqr_generic(Fe& r, const Fe& a) {
-  uint32_t t[16];
-  fm_mul512(t, a.v, a.v);
-  fm_reduce(r, t);
 }
 
 // a - b mod p for a < 2^256, b < p.
@@ -713,30 +487,14 @@ FM_DEV void fm_sub(Fe& r, const Fe& a, const Fe& b) {
       KHB_NOP
       "v_subb_co_u32_e32 %1, vcc, %1, %10, vcc\n\t"
       KHB_NOP
-#if KHB_RARE
       // the borrow into limb 2 (probability ~2^-32) is propagated in the rare branch
       "v_subb_co_u32_e32 %11, vcc, 0, %28, vcc"
-#else
-      "v_subbrev_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
-      KHB_NOP
-      "v_subbrev_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
-      KHB_NOP
-      "v_subbrev_co_u32_e32 %4, vcc, 0, %4, vcc\n\t"
-      KHB_NOP
-      "v_subbrev_co_u32_e32 %5, vcc, 0, %5, vcc\n\t"
-      KHB_NOP
-      "v_subbrev_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
-      KHB_NOP
-      "v_subbrev_co_u32_e32 %7, vcc, 0, %7, vcc\n\t"
-      "v_mov_b32 %11, 0"
-#endif
       : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]), "=&v"(d[6]), "=&v"(d[7]),
         "=&v"(m), "=&v"(k0), "=&v"(k1), "=&v"(b2)
       : "v"(a.v[0]), "v"(a.v[1]), "v"(a.v[2]), "v"(a.v[3]), "v"(a.v[4]), "v"(a.v[5]), "v"(a.v[6]), "v"(a.v[7]),
         "v"(b.v[0]), "v"(b.v[1]), "v"(b.v[2]), "v"(b.v[3]), "v"(b.v[4]), "v"(b.v[5]), "v"(b.v[6]), "v"(b.v[7]),
         "v"(0u)
       : "vcc");
-#if KHB_RARE
   if (fm_any(b2)) {      // b2 = 0xffffffff where the correction borrowed out of limb 1
     uint32_t bo = b2 & 1u;
 #pragma unroll
@@ -746,7 +504,6 @@ FM_DEV void fm_sub(Fe& r, const Fe& a, const Fe& b) {
       d[i] = t;
     }
   }
-#endif
 #pragma unroll
   for (int i = 0; i < 8; ++i) r.v[i] = d[i];
 }
@@ -815,7 +572,7 @@ FM_DEV void fm_add_lazy(Fe& r, const Fe& a, const Fe& b) {
         "v"(0u)
       : "vcc");
   // fold the carry as 2^256 = 0x1000003D1: limbs 0..1 always; the carry into limb 2 only behind
-  // the rare branch (KHB_RARE)
+  // the rare branch
   uint32_t c2;
   asm("v_mul_u32_u24_e32 %2, 0x3d1, %3\n\t"
       "v_add_co_u32_e32 %0, vcc, %0, %2\n\t"
@@ -826,11 +583,7 @@ FM_DEV void fm_add_lazy(Fe& r, const Fe& a, const Fe& b) {
       : "+v"(s[0]), "+v"(s[1]), "=&v"(c2)
       : "v"(c), "v"(0u)
       : "vcc");
-#if KHB_RARE
   if (fm_any(c2)) fm_propagate<2>(s, c2);
-#else
-  fm_propagate<2>(s, c2);
-#endif
 #pragma unroll
   for (int i = 0; i < 8; ++i) r.v[i] = s[i];
 }

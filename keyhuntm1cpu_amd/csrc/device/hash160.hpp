@@ -159,15 +159,6 @@ KHB_HD void hash160_compressed(uint32_t out[5], uint32_t prefix, const Fe& x) {
   ripemd160_of_sha(out, s);
 }
 
-// hash160 of both compressed keys 02 || x and 03 || x.  The two messages differ only in word 0, so
-// their SHA-256 schedules share W17, W19, W21 and the partial sums W[i-16] + s0(W[i-15]) + W[i-7] of
-// words 18..30; both compressions are inlined in one scope so the compiler computes those once
-// (gfx950: 4401 VALU for the pair vs 2 x 2249).
-KHB_HD void hash160_compressed_pair(uint32_t out2[5], uint32_t out3[5], const Fe& x) {
-  hash160_compressed(out2, 2u, x);
-  hash160_compressed(out3, 3u, x);
-}
-
 // hash160 of the uncompressed key 04 || x || y.
 KHB_HD void hash160_uncompressed(uint32_t out[5], const Fe& x, const Fe& y) {
   uint32_t w[16], s[8];

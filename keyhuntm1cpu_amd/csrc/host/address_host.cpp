@@ -453,6 +453,10 @@ void device_loop(AddrShared& S, int device) {
     S.stats.hits += st.n_cand;
     S.stats.degenerate += st.n_degenerate;
     S.stats.kernel_seconds += st.kernel_ms * 1e-3;
+    if (st.shader_mhz > 0) {
+      S.stats.shader_mhz_sum += st.shader_mhz;
+      S.stats.shader_mhz_n++;
+    }
     S.stats.found += found.size();
     if (S.cb.on_found)
       for (const AddrFound& f : found) S.cb.on_found(f);

@@ -69,6 +69,8 @@ struct AddrFound {
 struct AddrStats {
   uint64_t launches = 0, chunks = 0, keys = 0, hits = 0, found = 0, degenerate = 0;
   double kernel_seconds = 0;
+  double shader_mhz_sum = 0;       // sum of the launches' average shader clocks (khb_stats.shader_mhz)
+  uint64_t shader_mhz_n = 0;
 };
 
 struct AddrCallbacks {

@@ -50,6 +50,8 @@ struct SearchStats {
   double kernel_seconds = 0;       // summed over launches and devices (per-launch event time)
   double busy_seconds = 0;         // union of each device's launch intervals, summed over devices: the
                                    // device-busy time (two launches in flight overlap, so < kernel_seconds)
+  double shader_mhz_sum = 0;       // sum of the launches' average shader clocks (khb_stats.shader_mhz)
+  uint64_t shader_mhz_n = 0;
 };
 
 struct SearchCallbacks {

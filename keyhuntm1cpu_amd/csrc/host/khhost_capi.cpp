@@ -228,6 +228,7 @@ int khh_session_run(khh_session* s, const uint8_t* targets_xy, int n_targets, co
     stats_out[5] = st.launches;
     stats_out[6] = st.rescans;
     stats_out[7] = (uint64_t)(st.busy_seconds * 1e6);
+    stats_out[8] = st.shader_mhz_n ? (uint64_t)(1e3 * st.shader_mhz_sum / st.shader_mhz_n) : 0;
   }
   if (rc) set_err(err, errlen, e);
   return rc;
@@ -256,7 +257,7 @@ int khh_search(const khh_tables* t, const uint8_t* targets_xy, int n_targets, co
                char* err, size_t errlen) {
   khh_session* s = khh_session_open(t, devices, n_devices, lanes, chunks_per_batch, 0, err, errlen);
   if (!s) return KHB_ENODEV;
-  uint64_t st8[8] = {0};
+  uint64_t st8[9] = {0};
   int rc = khh_session_run(s, targets_xy, n_targets, start_be, end_be, max_chunks, 0, found, keys_be, st8, err,
                            errlen);
   if (stats_out) memcpy(stats_out, st8, 6 * sizeof(uint64_t));   // khh_search's stats hold 6
@@ -371,6 +372,7 @@ int khh_addr_search(const khh_addr* a, const uint8_t start_be[32], const uint8_t
     stats_out[3] = st.degenerate;
     stats_out[4] = (uint64_t)(st.kernel_seconds * 1e6);
     stats_out[5] = st.launches;
+    stats_out[6] = st.shader_mhz_n ? (uint64_t)(1e3 * st.shader_mhz_sum / st.shader_mhz_n) : 0;
   }
   if (rc) set_err(err, errlen, e);
   return rc;

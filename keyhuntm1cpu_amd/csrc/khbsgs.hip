@@ -266,8 +266,12 @@ ScanArgs make_args(khb_ctx* c, const Slot& S, uint32_t n_jobs, uint32_t group_be
   return A;
 }
 
-// kernel_ms and the launch's interval on the context's clock (khb_reset_epoch), from the slot's events.
+// kernel_ms and the launch's interval on the context's clock (khb_reset_epoch), from the slot's events;
+// the shader clock from the kernel's clock_probe samples.
 void launch_times(const khb_ctx* c, const Slot& S, khb_stats* st) {
+  uint64_t p[4];
+  memcpy(p, S.h_counters + 8, sizeof p);
+  st->shader_mhz = (p[3] > p[1] && p[2] > p[0]) ? (float)(100.0 * (double)(p[2] - p[0]) / (double)(p[3] - p[1])) : 0.f;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, S.ev0, S.ev1) != hipSuccess) ms = -1.f;
   st->kernel_ms = ms;
@@ -484,7 +488,8 @@ int khb_load_giant_table(khb_ctx* c, const uint8_t* gsn) {
   for (int i = 0; i < KHB_GIANT_TABLE; ++i) fe_sub(h.nx[i], zero, h.pt[i].x);
   if (!c->d_gsn) KHB_TRY(c, hipMalloc(&c->d_gsn, sizeof(h)));
   KHB_TRY(c, hipMemcpy(c->d_gsn, &h, sizeof(h), hipMemcpyHostToDevice));
-  std::vector<F9> h9(3 * KHB_GIANT_TABLE);
+#if KHB_F9WALK
+  std::vector<F9> h9(3 * KHB_GIANT_TABLE);     // the table in 9 x 29 limbs for the F9 walk (scan_f9.hpp)
   for (int i = 0; i < KHB_GIANT_TABLE; ++i) {
     f9_from_fe(h9[i], h.pt[i].x);
     f9_from_fe(h9[KHB_GIANT_TABLE + i], h.pt[i].y);
@@ -492,6 +497,7 @@ int khb_load_giant_table(khb_ctx* c, const uint8_t* gsn) {
   }
   if (!c->d_gsn9) KHB_TRY(c, hipMalloc(&c->d_gsn9, sizeof(F9) * h9.size()));
   KHB_TRY(c, hipMemcpy(c->d_gsn9, h9.data(), sizeof(F9) * h9.size(), hipMemcpyHostToDevice));
+#endif
   c->gofs_stale = true;
   return KHB_OK;
 }

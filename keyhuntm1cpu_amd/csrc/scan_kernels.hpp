@@ -8,7 +8,7 @@
 // Work decomposition:
 //   job   = one (chunk, target) pair; the host supplies its group-0 centre startP.
 //   item  = consecutive 1024-point groups of one job (scan_batch: 8 groups with two inversions).
-//   grid  = persistent: one residency of lanes takes items dynamically (KHB_DYN).
+//   grid  = persistent: one residency of lanes; each wave takes the next 64 items from a launch counter.
 // One lane's group maps 1:1 onto one reference group, so a collapsed batch inverse (dx == 0)
 // reproduces the reference's all-zero inverses exactly (IntGroup.cpp:36-58 + IntMod.cpp:497-500).
 #pragma once
@@ -29,32 +29,8 @@ struct AffPt {
   Fe x, y;
 };
 
-#ifndef KHB_PROBE_MODE
-#define KHB_PROBE_MODE 0          // 0 = product; 1..3 = perf experiments (tools/perf_variants.py)
-#endif
-#ifndef KHB_PROBE_BITS
-#define KHB_PROBE_BITS 1          // bloom bits per round trip in the drain (2 and 4 measured slower)
-#endif
-#ifndef KHB_GSN_SCALAR
-#define KHB_GSN_SCALAR 1          // GSn table through scalar loads
-#endif
-#ifndef KHB_PIPE
-#define KHB_PIPE 1                // walk_group software pipelining (bit 0 prefix prefetch, bit 1 paired gate loads)
-#endif
-#ifndef KHB_LDSCOUNT
-#define KHB_LDSCOUNT 1            // probe-queue count through an LDS-typed pointer (ds_* not flat_*)
-#endif
-#ifndef KHB_NT
-#define KHB_NT 0                  // prefix scratch through non-temporal loads/stores
-#endif
-#ifndef KHB_FUSE
-#define KHB_FUSE 1                // -m bsgs walk: x = s^2 + nu fused into the squaring's reduction
-#endif
 #ifndef KHB_GATE1
 #define KHB_GATE1 25              // default log2 bytes of the stage-1 fold of a larger level-0 gate (0 = none)
-#endif
-#ifndef KHB_DYN
-#define KHB_DYN 1                 // scan_batch kernels: dynamic per-wave work items (launch counter)
 #endif
 #ifndef KHB_WAVES_PER_SIMD
 #define KHB_WAVES_PER_SIMD 4      // occupancy target of k_giant_scan (launch bounds); w4 measured best
@@ -93,38 +69,19 @@ constexpr bool is_dump(int m) { return m == kDump || m == kAddrDump || m == kBab
 #ifndef KHB_ADDR_WAVES_PER_SIMD
 #define KHB_ADDR_WAVES_PER_SIMD KHB_WAVES_PER_SIMD   // occupancy target of the -m address hash kernels
 #endif
-#ifndef KHB_ADDR_PAIR
-#define KHB_ADDR_PAIR 0            // -m address 02/03 hashes in one scope (shared SHA-256 schedule words)
-#endif
 constexpr int waves_per_simd(int m) { return is_addr(m) ? KHB_ADDR_WAVES_PER_SIMD : KHB_WAVES_PER_SIMD; }
 constexpr uint32_t kHalf = KHB_GROUP / 2;            // 512
 constexpr uint32_t kCandCap = 1u << 20;
 constexpr uint32_t kAddrHitCap = 1u << 18;
 constexpr uint32_t kDegenCap = 4096;
-constexpr size_t kCounterBytes = 32;                 // ScanArgs::counters
+constexpr size_t kCounterBytes = 64;                 // ScanArgs::counters
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-// Prefix-scratch stream (written once by the forward pass, read once by the walk): with
-// KHB_NT the accesses are non-temporal, so the stream does not evict the level-0 gate from L2.
-__device__ __forceinline__ void scr_st(Fe* p, const Fe& v) {
-#if KHB_NT
-  v4u* q = reinterpret_cast<v4u*>(p);
-  __builtin_nontemporal_store(v4u{v.v[0], v.v[1], v.v[2], v.v[3]}, q);
-  __builtin_nontemporal_store(v4u{v.v[4], v.v[5], v.v[6], v.v[7]}, q + 1);
-#else
-  *p = v;
-#endif
-}
-__device__ __forceinline__ Fe scr_ld(const Fe* p) {
-#if KHB_NT
-  const v4u* q = reinterpret_cast<const v4u*>(p);
-  const v4u a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1);
-  return Fe{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
-#else
-  return *p;
-#endif
-}
+// Prefix-scratch stream (written once by the forward pass, read once by the walk).  Non-temporal
+// accesses were measured slower (profiles/r01_gate_experiments_raw.txt), so these are plain.
+__device__ __forceinline__ void scr_st(Fe* p, const Fe& v) { *p = v; }
+__device__ __forceinline__ Fe scr_ld(const Fe* p) { return *p; }
 
 struct ScanArgs {
   const uint8_t* __restrict__ bloom;
@@ -137,8 +94,10 @@ struct ScanArgs {
   Fe* __restrict__ scratch;            // prefix products [512][lanes]
   khb_cand* __restrict__ cand;
   khb_degenerate* __restrict__ degen;
-  uint32_t* __restrict__ counters;     // [0] candidates [1] degenerate groups [2] work-item cursor (KHB_DYN)
+  uint32_t* __restrict__ counters;     // [0] candidates [1] degenerate groups [2] work-item cursor (dynamic items)
                                        // [4..5] groups walked (u64, count_walked)
+                                       // [8..15] shader clock probe (clock_probe): memtime, realtime at the
+                                       // first wave's start, then at its end (u64 each)
   uint8_t* __restrict__ xdump;         // dump modes only
   uint32_t* __restrict__ ahits;        // -m address hits: {job, group, t, kind} x ahit_cap
   uint32_t ahit_cap;
@@ -197,11 +156,7 @@ struct ProbeQueue {
   // this wave's queued-entry count, typed as an LDS pointer: through a generic (flat) pointer
   // every count access was a flat_load/flat_store, which counts against vmcnt AND lgkmcnt and
   // made each one wait for all outstanding vector-memory operations (the prefetched prefix).
-#if KHB_LDSCOUNT
   volatile __attribute__((address_space(3))) uint32_t* n;
-#else
-  volatile uint32_t* n;
-#endif
 };
 
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
@@ -234,7 +189,7 @@ __device__ __forceinline__ void q_drain(const ScanArgs& A, ProbeQueue& Q, uint32
       uint64_t w[4];
       x_words(w, x);
       // the whole level-1 check (bit 0 again for ungated pushes: the first hash is not queued)
-      if (bloom_full<KHB_PROBE_BITS>(sub_bloom(A.bloom, A.geom, x), A.geom, w, xxh64_32(w, KHB_BLOOM_SEED)))
+      if (bloom_full<1>(sub_bloom(A.bloom, A.geom, x), A.geom, w, xxh64_32(w, KHB_BLOOM_SEED)))
         emit_cand(A, job, step);
     }
     asm volatile("" ::: "memory");
@@ -265,19 +220,9 @@ __device__ __forceinline__ uint32_t gate_bits(const ScanArgs& A, const Fe& x) {
   return b0 | (b1 << 6) | (b2 << 12);
 }
 
-// All three packed bits set in the 64-bit block (lo, hi)?  KHB_GATE_SHR64: one 64-bit shift per bit
-// (v_lshrrev_b64) instead of a word select and a 32-bit shift: 28 instead of 38 VALU per walk step,
-// measured no faster (47.39 vs 47.54 G steps/s, profiles/r02p_gate_shr64_ab.txt), so off.
-#ifndef KHB_GATE_SHR64
-#define KHB_GATE_SHR64 0
-#endif
+// All three packed bits set in the 64-bit block (lo, hi)?  (One 64-bit shift per bit instead of the
+// word select measured no faster, profiles/r02p_gate_shr64_ab.txt.)
 __device__ __forceinline__ bool gate_block_pass(uint32_t lo, uint32_t hi, uint32_t bits) {
-#if KHB_GATE_SHR64
-  const uint64_t blk = ((uint64_t)hi << 32) | lo;
-  const uint32_t r = (uint32_t)(blk >> (bits & 63u)) & (uint32_t)(blk >> ((bits >> 6) & 63u)) &
-                     (uint32_t)(blk >> ((bits >> 12) & 63u));
-  return r & 1u;
-#else
   uint32_t r = 1u;
 #pragma unroll
   for (int p = 0; p < 3; ++p) {
@@ -285,7 +230,6 @@ __device__ __forceinline__ bool gate_block_pass(uint32_t lo, uint32_t hi, uint32
     r &= ((b & 32u) ? hi : lo) >> (b & 31u);
   }
   return r & 1u;
-#endif
 }
 
 // A gate test: x's 64-bit block of the map (one 8-byte load: a single cache line per x whatever
@@ -295,19 +239,8 @@ struct GatePend {
   __device__ __forceinline__ bool pass() const { return gate_block_pass(lo, hi, bits); }
 };
 
-#ifndef KHB_GATE_EARLY
-#define KHB_GATE_EARLY 0          // 1 = kScanG issues x1's gate load before computing x2 (experiment)
-#endif
-#ifndef KHB_GATE_NT
-#define KHB_GATE_NT 0             // 1 = gate blocks through non-temporal loads (experiment)
-#endif
 __device__ __forceinline__ GatePend gate_issue(const ScanArgs& A, const Fe& x) {
-#if KHB_GATE_NT
-  const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(A.gate) + (x.v[0] & A.gate_mask));
-  const uint2 w = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
-#else
   const uint2 w = reinterpret_cast<const uint2*>(A.gate)[x.v[0] & A.gate_mask];
-#endif
   return GatePend{w.x, w.y, gate_bits(A, x)};
 }
 
@@ -341,19 +274,6 @@ __device__ __forceinline__ void gate_pair(const ScanArgs& A, ProbeQueue& Q, cons
   q_drain(A, Q, kDrainAt);
 }
 
-// kScanG with the loads already issued (KHB_GATE_EARLY): x1's block is requested as soon as x1 exists,
-// so its latency hides behind x2's multiply and square.
-__device__ __forceinline__ void gate_pair_pend(const ScanArgs& A, ProbeQueue& Q, const GatePend& q1, const Fe& x1,
-                                               uint32_t step1, const GatePend& q2, const Fe& x2, uint32_t step2,
-                                               uint32_t job) {
-  const bool h1 = q1.pass(), h2 = q2.pass();
-  if (__ballot(h1 || h2) == 0) return;
-  q_push(Q, h1, x1, job, step1);
-  q_drain(A, Q, kDrainAt);
-  q_push(Q, h2, x2, job, step2);
-  q_drain(A, Q, kDrainAt);
-}
-
 // Gate bits of x (blocked gate), or without a gate L1 bit 0 (a = the first XXH64).
 __device__ __forceinline__ bool first_bit(const ScanArgs& A, const Fe& x, uint64_t& a) {
   if (A.gate) {
@@ -374,37 +294,10 @@ __device__ __forceinline__ void probe(const ScanArgs& A, ProbeQueue& Q, const Fe
     uint8_t* o = A.xdump + ((uint64_t)(j - A.group_begin) * KHB_GROUP + t) * 32;
     fe_to_be(o, x);
   } else {
-#if KHB_PROBE_MODE == 0
     uint64_t a;
     const bool hit = first_bit(A, x, a);
     q_push(Q, hit, x, job, j * KHB_GROUP + t);
     q_drain(A, Q, kDrainAt);
-#elif KHB_PROBE_MODE == 1      // perf experiment: first hash only, no bloom access
-    uint64_t w[4];
-    x_words(w, x);
-    if (xxh64_32(w, KHB_BLOOM_SEED) == 0x0123456789abcdefull) emit_cand(A, job, j * KHB_GROUP + t);
-#elif KHB_PROBE_MODE == 2      // perf experiment: first hash + first bit only
-    uint64_t w[4];
-    x_words(w, x);
-    const uint64_t a = xxh64_32(w, KHB_BLOOM_SEED);
-    const uint8_t* bf = sub_bloom(A.bloom, A.geom, x);
-    const uint64_t pos = mod_bits(a, A.geom);
-    if ((bf[pos >> 3] >> (pos & 7)) & 1u & (a == 0x0123456789abcdefull)) emit_cand(A, job, j * KHB_GROUP + t);
-#elif KHB_PROBE_MODE == 4      // perf experiment: first hash + one random bit of a 4 MiB table
-    uint64_t w[4];
-    x_words(w, x);
-    const uint64_t a = xxh64_32(w, KHB_BLOOM_SEED);
-    const uint8_t byte = A.bloom[a >> 42];
-    if (((byte >> ((a >> 39) & 7)) & 1u) & (a == 0x0123456789abcdefull)) emit_cand(A, job, j * KHB_GROUP + t);
-#elif KHB_PROBE_MODE == 5      // perf experiment: as 4 with a 2 MiB table
-    uint64_t w[4];
-    x_words(w, x);
-    const uint64_t a = xxh64_32(w, KHB_BLOOM_SEED);
-    const uint8_t byte = A.bloom[a >> 43];
-    if (((byte >> ((a >> 40) & 7)) & 1u) & (a == 0x0123456789abcdefull)) emit_cand(A, job, j * KHB_GROUP + t);
-#else                          // perf experiment: no probe at all
-    if (x.v[0] == 0x01234567u && x.v[1] == 0x89abcdefu) emit_cand(A, job, j * KHB_GROUP + t);
-#endif
   }
 }
 
@@ -413,7 +306,6 @@ __device__ __forceinline__ void probe(const ScanArgs& A, ProbeQueue& Q, const Fe
 template <bool DUMP>
 __device__ __forceinline__ void probe_pair(const ScanArgs& A, ProbeQueue& Q, const Fe& x1, const Fe& x2,
                                            uint32_t job, uint32_t j, uint32_t t1, uint32_t t2) {
-#if KHB_PROBE_MODE == 0
   if (!DUMP) {
     uint64_t a1, a2;
     const bool h1 = first_bit(A, x1, a1);
@@ -424,17 +316,15 @@ __device__ __forceinline__ void probe_pair(const ScanArgs& A, ProbeQueue& Q, con
     q_drain(A, Q, kDrainAt);
     return;
   }
-#endif
   probe<DUMP>(A, Q, x1, job, j, t1);
   probe<DUMP>(A, Q, x2, job, j, t2);
 }
 
-// GSn / _2GSn rows (wave-uniform index).  With KHB_GSN_SCALAR the table is read through the
-// constant address space, so rows arrive by scalar loads into SGPRs (lgkmcnt) instead of taking
-// 16 VGPRs and four vector-memory slots per backward step.
+// GSn / _2GSn rows (wave-uniform index), read through the constant address space, so rows arrive
+// by scalar loads into SGPRs (lgkmcnt) instead of taking 16 VGPRs and four vector-memory slots per
+// backward step.
 struct GsnTable {
   const AffPt* p;
-#if KHB_GSN_SCALAR
   typedef const __attribute__((address_space(4))) uint32_t* CW;
   __device__ __forceinline__ Fe ld(uint32_t word) const {
     CW w = (CW)p + word;
@@ -447,11 +337,6 @@ struct GsnTable {
   __device__ __forceinline__ AffPt pt(uint32_t i) const { return AffPt{ld(16 * i), ld(16 * i + 8)}; }
   // p - GSn[i].x (0 for x = 0), stored after the 513 points (khb_load_giant_table)
   __device__ __forceinline__ Fe nx(uint32_t i) const { return ld(16 * KHB_GIANT_TABLE + 8 * i); }
-#else
-  __device__ __forceinline__ Fe x(uint32_t i) const { return p[i].x; }
-  __device__ __forceinline__ AffPt pt(uint32_t i) const { return p[i]; }
-  __device__ __forceinline__ Fe nx(uint32_t i) const { return reinterpret_cast<const Fe*>(p + KHB_GIANT_TABLE)[i]; }
-#endif
 };
 
 // -m address handling of one point (keyhunt.cpp:2716-2937, BTC, no endomorphism): hash160 of
@@ -475,18 +360,11 @@ __device__ __forceinline__ void addr_point(const ScanArgs& A, const Fe& x, const
       }
     };
     if constexpr (MODE == kAddrC || MODE == kAddrB) {
-#if KHB_ADDR_PAIR
-      uint32_t h3[5];
-      hash160_compressed_pair(h, h3, x);
-      if (bloom_check20(A.bloom, A.geom, h)) emit(0);
-      if (bloom_check20(A.bloom, A.geom, h3)) emit(1);
-#else
 #pragma unroll 1
       for (uint32_t pre = 2; pre <= 3; ++pre) {
         hash160_compressed(h, pre, x);
         if (bloom_check20(A.bloom, A.geom, h)) emit(pre - 2);
       }
-#endif
     }
     if constexpr (MODE == kAddrU || MODE == kAddrB) {
       hash160_uncompressed(h, x, y);
@@ -569,15 +447,15 @@ __device__ __forceinline__ void walk_group(const ScanArgs& A, ProbeQueue& Q, con
   const uint32_t S = A.stride;
   const GsnTable gsn{A.gsn};
   Fe pre, dx;
-  // KHB_PIPE bit 0: the prefix for step i-1 is loaded during step i, so its HBM latency hides
-  // behind a whole step's arithmetic instead of being waited for right after the load.
-  constexpr bool PREFETCH = (KHB_PIPE & 1) && is_scan(MODE);
+  // scan modes: the prefix for step i-1 is loaded during step i, so its HBM latency hides behind a
+  // whole step's arithmetic instead of being waited for right after the load.
+  constexpr bool PREFETCH = is_scan(MODE);
   // The load goes into `pre` itself right after its last use (no loop-carried copy: a copy at the
   // loop latch would make the wave wait for the load there).
   if (PREFETCH) pre = scr[(size_t)(kHalf - 2) * S];
-  // KHB_FUSE (-m bsgs x-only walks): C.x is carried as negCx = p - C.x, so dx = GSn.x + negCx and
+  // -m bsgs x-only walks: C.x is carried as negCx = p - C.x, so dx = GSn.x + negCx and
   // x = s^2 + (negCx - GSn.x) need no separate modular subtraction of the centre.
-  constexpr bool FUSED = KHB_FUSE && (MODE == kScan || MODE == kDump);
+  constexpr bool FUSED = MODE == kScan || MODE == kDump;
   Fe negCx;
   if constexpr (FUSED) {
     Fe p;
@@ -613,7 +491,7 @@ __device__ __forceinline__ void walk_group(const ScanArgs& A, ProbeQueue& Q, con
         fm_mul(s, s, idx);
         fm_sqr_add(x2, s, u);
         x_out<MODE>(A, x2);
-        if constexpr ((KHB_PIPE & 2) && is_scan(MODE))
+        if constexpr (is_scan(MODE))          // both x before either probe load is issued
           asm volatile("" ::"v"(x1.v[0]), "v"(x2.v[0]), "v"(x1.v[7]), "v"(x2.v[7]) : "memory");
         probe_pair<DUMP>(A, Q, x1, x2, job, j, kHalf - 1 - (uint32_t)i, kHalf + 1 + (uint32_t)i);
       } else {
@@ -657,7 +535,7 @@ __device__ __forceinline__ void walk_group(const ScanArgs& A, ProbeQueue& Q, con
         addr_point<MODE>(A, x1, y1, job, j, kHalf - 1 - (uint32_t)i);
         addr_point<MODE>(A, x2, y2, job, j, kHalf + 1 + (uint32_t)i);
       } else {
-        if constexpr ((KHB_PIPE & 2) && MODE == kScan)   // both x before either gate load is issued
+        if constexpr (MODE == kScan)                       // both x before either probe load is issued
           asm volatile("" ::"v"(x1.v[0]), "v"(x2.v[0]), "v"(x1.v[7]), "v"(x2.v[7]) : "memory");
         probe_pair<DUMP>(A, Q, x1, x2, job, j, kHalf - 1 - (uint32_t)i, kHalf + 1 + (uint32_t)i);
       }
@@ -679,7 +557,7 @@ __device__ __forceinline__ void walk_group(const ScanArgs& A, ProbeQueue& Q, con
 }
 
 // walk_group for kScanG (-m bsgs with a level-0 gate), the product path: same points, same order,
-// with the fused x-only arithmetic (x = s^2 + nu, KHB_FUSE), the prefix of step i-1 loaded right
+// with the fused x-only arithmetic (x = s^2 + nu), the prefix of step i-1 loaded right
 // after step i's last use of the prefix register (its HBM latency hides behind a whole step), and
 // each step's two x gate-tested together (gate_pair).  The first step is peeled and the prefix
 // load is unconditional, so the loop body issues the same vector-memory sequence every time and
@@ -731,18 +609,6 @@ __device__ __forceinline__ void walk_group_g(const ScanArgs& A, ProbeQueue& Q, c
     fm_mul(s, s, idx);
     fm_sqr_add(x1, s, u);
     x_out<kScanG>(A, x1);
-#if KHB_GATE_EARLY
-    if constexpr (!STAGE1) {
-      const GatePend q1 = gate_issue(A, x1);
-      fm_add_lazy(s, g.y, negCy);             // GSn.y - C.y
-      fm_mul(s, s, idx);
-      fm_sqr_add(x2, s, u);
-      x_out<kScanG>(A, x2);
-      const GatePend q2 = gate_issue(A, x2);
-      gate_pair_pend(A, Q, q1, x1, base + kHalf - 1 - (uint32_t)i, q2, x2, base + kHalf + 1 + (uint32_t)i, job);
-      continue;
-    }
-#endif
     fm_add_lazy(s, g.y, negCy);               // GSn.y - C.y
     fm_mul(s, s, idx);
     fm_sqr_add(x2, s, u);
@@ -998,431 +864,9 @@ __device__ __forceinline__ uint32_t scan_batch(const ScanArgs& A, ProbeQueue& Q,
   return walked;
 }
 
-// ---- the product walk in 9 x 29-bit limbs (kScanG, kScanG1, kDumpG; device/fe29.hpp) -----------
-
-// GSn in 9 x 29 limbs (khb_load_giant_table): x of rows 0..512, then y, then p - x; wave-uniform
-// rows through the constant address space (scalar loads), as GsnTable.
-struct Gsn9 {
-  const F9* p;
-  typedef const __attribute__((address_space(4))) uint32_t* CW;
-  __device__ __forceinline__ F9 ld(uint32_t row) const {
-    CW w = (CW)p + 9 * row;
-    F9 r;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) r.v[k] = w[k];
-    return r;
-  }
-  __device__ __forceinline__ F9 x(uint32_t i) const { return ld(i); }
-  __device__ __forceinline__ F9 y(uint32_t i) const { return ld(KHB_GIANT_TABLE + i); }
-  __device__ __forceinline__ F9 nx(uint32_t i) const { return ld(2 * KHB_GIANT_TABLE + i); }
-};
-
-// Lane-private scratch of the F9 path: 36 bytes per lane per entry, split by limbs so that every
-// access is an aligned, fully coalesced wave-wide block: entry e occupies 36 * lanes bytes at
-// e * 36 * lanes, limbs 0-3 of all lanes (16 B each), then limbs 4-7, then limb 8 (4 B each).  An
-// 8 x 32 value (centres) uses the first two parts.
-struct Scr9 {
-  uint8_t* s;
-  size_t S;
-  uint32_t lane;
-  __device__ __forceinline__ v4u* p0(uint32_t e) const { return reinterpret_cast<v4u*>(s + (size_t)e * 36 * S) + lane; }
-  __device__ __forceinline__ v4u* p1(uint32_t e) const {
-    return reinterpret_cast<v4u*>(s + (size_t)e * 36 * S + 16 * S) + lane;
-  }
-  __device__ __forceinline__ uint32_t* p2(uint32_t e) const {
-    return reinterpret_cast<uint32_t*>(s + (size_t)e * 36 * S + 32 * S) + lane;
-  }
-  __device__ __forceinline__ F9 ld9(uint32_t e) const {
-    const v4u a = *p0(e), b = *p1(e);
-    return F9{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, *p2(e)}};
-  }
-  __device__ __forceinline__ void st9(uint32_t e, const F9& v) const {
-    *p0(e) = v4u{v.v[0], v.v[1], v.v[2], v.v[3]};
-    *p1(e) = v4u{v.v[4], v.v[5], v.v[6], v.v[7]};
-    *p2(e) = v.v[8];
-  }
-  __device__ __forceinline__ Fe ldfe(uint32_t e) const {
-    const v4u a = *p0(e), b = *p1(e);
-    return Fe{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
-  }
-  __device__ __forceinline__ void stfe(uint32_t e, const Fe& v) const {
-    *p0(e) = v4u{v.v[0], v.v[1], v.v[2], v.v[3]};
-    *p1(e) = v4u{v.v[4], v.v[5], v.v[6], v.v[7]};
-  }
-};
-
-__device__ __forceinline__ F9 f9_small(uint32_t v) {
-  F9 r;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) r.v[k] = k ? 0u : v;
-  return r;
-}
-
-// Low 64 bits of canonical x (the gate's words, f9_gate_words); the rare inputs whose fast words
-// are not exact take the full conversion behind a wave-uniform branch.
-__device__ __forceinline__ void gate_words(const F9& x, uint32_t& w0, uint32_t& w1) {
-  bool rare;
-  f9_gate_words(w0, w1, rare, x);
-  if (__builtin_expect(__ballot(rare) != 0, 0)) {
-    if (rare) {
-      Fe c;
-      f9_to_fe(c, x);
-      w0 = c.v[0];
-      w1 = c.v[1];
-    }
-  }
-}
-
-__device__ __forceinline__ uint32_t gate_bits_w(const ScanArgs& A, uint32_t w1) {
-  const uint32_t b0 = w1 & 63u, b1 = A.gate_probes > 1 ? (w1 >> 6) & 63u : b0;
-  const uint32_t b2 = A.gate_probes > 2 ? (w1 >> 12) & 63u : b1;
-  return b0 | (b1 << 6) | (b2 << 12);
-}
-
-// The gate test of one x from its canonical words: the 64-bit block load is issued here and waited
-// for in pass(), so a step issues both x's loads before testing either (GatePend).  With the stage-1
-// fold the fold's block is tested first and the full gate's block is read only for its survivors.
-template <bool STAGE1>
-struct Gate9 {
-  uint32_t lo, hi, bits, w0;
-  __device__ __forceinline__ void issue(const ScanArgs& A, uint32_t a0, uint32_t a1) {
-    const uint2 w = reinterpret_cast<const uint2*>(STAGE1 ? A.gate1 : A.gate)[a0 & (STAGE1 ? A.gate1_mask : A.gate_mask)];
-    lo = w.x;
-    hi = w.y;
-    bits = gate_bits_w(A, a1);
-    w0 = a0;
-  }
-};
-
-template <bool STAGE1>
-__device__ __forceinline__ void gate_resolve(const ScanArgs& A, const Gate9<STAGE1>& g1, bool has2,
-                                             const Gate9<STAGE1>& g2, bool& h1, bool& h2) {
-  if constexpr (STAGE1) {
-    const bool s1 = gate_block_pass(g1.lo, g1.hi, g1.bits), s2 = has2 && gate_block_pass(g2.lo, g2.hi, g2.bits);
-    h1 = h2 = false;
-    if (__ballot(s1 || s2) == 0) return;
-    uint2 w1 = make_uint2(0u, 0u), w2 = make_uint2(0u, 0u);
-    if (s1) w1 = reinterpret_cast<const uint2*>(A.gate)[g1.w0 & A.gate_mask];
-    if (s2) w2 = reinterpret_cast<const uint2*>(A.gate)[g2.w0 & A.gate_mask];
-    h1 = s1 && gate_block_pass(w1.x, w1.y, g1.bits);
-    h2 = s2 && gate_block_pass(w2.x, w2.y, g2.bits);
-  } else {
-    h1 = gate_block_pass(g1.lo, g1.hi, g1.bits);
-    h2 = has2 && gate_block_pass(g2.lo, g2.hi, g2.bits);
-  }
-}
-
-__device__ __forceinline__ void x_dump9(const ScanArgs& A, const F9& x, uint32_t step) {
-  Fe c;
-  f9_to_fe(c, x);
-  fe_to_be(A.xdump + ((uint64_t)step - (uint64_t)A.group_begin * KHB_GROUP) * 32, c);
-}
-
-// walk_group_g in 9 x 29 limbs: the same points in the same order (pts[511 - i] = C - GSn[i],
-// pts[513 + i] = C + GSn[i], pts[512] = C), x = s^2 + nu with nu = (p - GSn.x) + (p - C.x), the
-// prefix of step i - 1 loaded right after step i's last use of the prefix register.  inv is the
-// inverse of the group's 512 dx; sg.ld9(e0 + e) is prefix e of this group.
-// Register budget (128 VGPRs at 4 waves/SIMD): the first x of a step is reduced to its gate words
-// and its gate load before the second is computed, and is recomputed (from idx) only for a gate
-// survivor; -C.y is not held (f9_add_neg forms GSn.y - C.y from C.y).
-// p - C.x (which = 0) and C.y (which = 1) of the walked group: parked in LDS by walk_group_g9 and
-// read where used (volatile: no hoisting back into registers).
-#ifndef KHB_CN_VOLATILE
-#define KHB_CN_VOLATILE 1
+#if KHB_F9WALK
+#include "scan_f9.hpp"        // the gated walk in 9 x 29-bit limbs (alternative build, `make variants`)
 #endif
-#ifndef KHB_CN_LDS
-#define KHB_CN_LDS 1              // F9 walk: p - C.x and C.y parked in LDS (0: held in registers)
-#endif
-__device__ __forceinline__ F9 cn_load(const ProbeQueue& Q, int which) {
-  uint32_t wl = threadIdx.x & 63u;
-  F9 r;
-#if KHB_CN_VOLATILE
-#pragma unroll
-  for (int k = 0; k < 9; ++k) r.v[k] = Q.cn[(9 * which + k) * 64 + wl];
-#else
-  // a plain LDS load at an address the compiler cannot prove loop-invariant: it may issue the load
-  // early, but cannot hoist it out of the walk loop into 9 long-lived registers
-  asm volatile("" : "+v"(wl));
-  const __attribute__((address_space(3))) uint32_t* c = (const __attribute__((address_space(3))) uint32_t*)Q.cn;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) r.v[k] = c[(9 * which + k) * 64 + wl];
-#endif
-  return r;
-}
-
-template <int MODE>
-__device__ __forceinline__ void walk_group_g9(const ScanArgs& A, ProbeQueue& Q, const AffPt& C, F9 inv,
-                                              uint32_t job, uint32_t j, const Scr9& sg, uint32_t e0) {
-  constexpr bool STAGE1 = MODE == kScanG1;
-  const Gsn9 g9{A.gsn9};
-  const uint32_t base = j * KHB_GROUP;
-#if KHB_CN_LDS
-  {
-    Fe p, t;
-    F9 ncx, cy;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) p.v[k] = k == 0 ? KHB_P0 : (k == 1 ? KHB_P1 : 0xFFFFFFFFu);
-    fm_sub(t, p, C.x);
-    f9_from_fe(ncx, t);
-    f9_from_fe(cy, C.y);
-    const uint32_t wl = threadIdx.x & 63u;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-      Q.cn[k * 64 + wl] = ncx.v[k];
-      Q.cn[(9 + k) * 64 + wl] = cy.v[k];
-    }
-  }
-#define ncx cn_load(Q, 0)
-#define cy cn_load(Q, 1)
-#else
-  F9 ncx, cy;
-  {
-    Fe p, t;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) p.v[k] = k == 0 ? KHB_P0 : (k == 1 ? KHB_P1 : 0xFFFFFFFFu);
-    fm_sub(t, p, C.x);
-    f9_from_fe(ncx, t);
-    f9_from_fe(cy, C.y);
-  }
-#endif
-  F9 pre = sg.ld9(e0 + kHalf - 2);
-  F9 idx, dx, s, x;
-  {   // step 511: pts[0] = C - GSn[511] only
-    f9_mul(idx, inv, pre);
-    pre = sg.ld9(e0 + kHalf - 3);
-    f9_add(dx, g9.x(kHalf - 1), ncx);
-    f9_mul(inv, inv, dx);
-    f9_add(s, g9.y(kHalf - 1), cy);
-    f9_mul(s, s, idx);
-    f9_sqr(x, s);
-    f9_add(x, x, g9.nx(kHalf - 1));
-    f9_add(x, x, ncx);
-    if constexpr (MODE == kDumpG) {
-      x_dump9(A, x, base);
-    } else {
-      uint32_t a0, a1;
-      gate_words(x, a0, a1);
-      Gate9<STAGE1> q;
-      q.issue(A, a0, a1);
-      bool h1, h2;
-      gate_resolve<STAGE1>(A, q, false, q, h1, h2);
-      if (__ballot(h1) != 0) {
-        Fe c = Fe{};
-        if (h1) f9_to_fe(c, x);
-        q_push(Q, h1, c, job, base);
-        q_drain(A, Q, kDrainAt);
-      }
-    }
-  }
-  for (int i = (int)kHalf - 2; i >= 0; --i) {
-    if (i > 0) {
-      f9_mul(idx, inv, pre);
-      pre = sg.ld9(e0 + (i >= 2 ? i - 2 : 0));    // i = 1: a harmless reload of prefix 0
-      f9_add(dx, g9.x(i), ncx);
-      f9_mul(inv, inv, dx);
-    } else {
-      idx = inv;
-    }
-    const uint32_t t1 = base + kHalf - 1 - (uint32_t)i, t2 = base + kHalf + 1 + (uint32_t)i;
-    // C - GSn[i]: s' = (GSn.y + C.y) / dx, x = s'^2 + nu
-    f9_add(s, g9.y(i), cy);
-    f9_mul(s, s, idx);
-    f9_sqr(x, s);
-    f9_add(x, x, g9.nx(i));
-    f9_add(x, x, ncx);
-    Gate9<STAGE1> q1, q2;
-    if constexpr (MODE == kDumpG) {
-      x_dump9(A, x, t1);
-    } else {
-      uint32_t a0, a1;
-      gate_words(x, a0, a1);
-      q1.issue(A, a0, a1);
-    }
-    // C + GSn[i]: s = (GSn.y - C.y) / dx
-    f9_add_neg(s, g9.y(i), cy);
-    f9_mul(s, s, idx);
-    f9_sqr(x, s);
-    f9_add(x, x, g9.nx(i));
-    f9_add(x, x, ncx);
-    if constexpr (MODE == kDumpG) {
-      x_dump9(A, x, t2);
-    } else {
-      uint32_t a0, a1;
-      gate_words(x, a0, a1);
-      q2.issue(A, a0, a1);
-      bool h1, h2;
-      gate_resolve<STAGE1>(A, q1, true, q2, h1, h2);
-      // ~0.04 % of x pass: their canonical forms go to the queue, one x at a time (the second x
-      // first, then the first recomputed from idx), so this rare path needs few registers
-      if (__ballot(h2) != 0) {
-        Fe c = Fe{};
-        if (h2) f9_to_fe(c, x);
-        q_push(Q, h2, c, job, t2);
-        q_drain(A, Q, kDrainAt);
-      }
-      if (__ballot(h1) != 0) {
-        Fe c = Fe{};
-        if (h1) {
-          f9_add(s, g9.y(i), cy);
-          f9_mul(s, s, idx);
-          f9_sqr(x, s);
-          f9_add(x, x, g9.nx(i));
-          f9_add(x, x, ncx);
-          f9_to_fe(c, x);
-        }
-        q_push(Q, h1, c, job, t1);
-        q_drain(A, Q, kDrainAt);
-      }
-    }
-  }
-#if KHB_CN_LDS
-#undef ncx
-#undef cy
-#endif
-  if constexpr (MODE == kDumpG) {
-    fe_to_be(A.xdump + ((uint64_t)(j - A.group_begin) * KHB_GROUP + kHalf) * 32, C.x);
-  } else {
-    probe<false>(A, Q, C.x, job, j, kHalf);      // the centre, pts[512] (canonical)
-  }
-}
-
-// scan_batch for the F9 walk: step 0 (centres) in 8 x 32 as scan_batch; steps 1-3 (forward
-// prefix products, one inversion for the batch, the walks) in 9 x 29 limbs.  Scratch entries are
-// 36 bytes (Scr9), numbered as in scan_batch: g*512 + i prefixes, g*512 + 511 = T_g then inv(T_g),
-// kBatch*512 + 2g (+1) = C_g.x (.y), kBatch*514 + g = chained products.
-template <int MODE>
-__device__ __forceinline__ uint32_t scan_batch9(const ScanArgs& A, ProbeQueue& Q, uint32_t job, uint32_t g0,
-                                                uint32_t g1, uint32_t lane) {
-  const Scr9 sr{reinterpret_cast<uint8_t*>(A.scratch), (size_t)A.stride, lane};
-  const Gsn9 g9{A.gsn9};
-  const GsnTable gsn{A.gsn};
-  const uint32_t nb = g1 - g0;
-  constexpr uint32_t SC = kBatch * kHalf, SQ = kBatch * (kHalf + 2);
-  const AffPt P = A.centres[job];
-  // 0. centres (as scan_batch, 8 x 32)
-  uint32_t skip = 0;
-  {
-    Fe acc;
-    for (uint32_t g = 0; g < nb; ++g) {
-      const uint32_t jg = g0 + g;
-      Fe d = fe_small(1);
-      if (jg != 0) {
-        fm_sub(d, A.gofs[jg].x, P.x);
-        Fe dc;
-        fm_canon(dc, d);
-        if (fe_is_zero(dc)) {
-          d = fe_small(1);
-          skip |= 1u << g;
-          if (MODE != kDumpG) {
-            const uint32_t k = atomicAdd(&A.counters[1], 1u);
-            if (k < A.degen_cap) A.degen[k] = khb_degenerate{job, jg | 0x80000000u};
-          }
-        }
-      } else {
-        skip |= 1u << g;
-      }
-      if (g == 0) acc = d; else fm_mul(acc, acc, d);
-      sr.stfe(SQ + g, acc);
-    }
-    Fe inv;
-    fm_inv(inv, acc);
-    for (int g = (int)nb - 1; g >= 0; --g) {
-      const uint32_t jg = g0 + (uint32_t)g;
-      const AffPt O = A.gofs[jg];
-      Fe ig;
-      if (g > 0) {
-        fm_mul(ig, inv, sr.ldfe(SQ + g - 1));
-        Fe d = fe_small(1);
-        if (!((skip >> g) & 1u)) fm_sub(d, O.x, P.x);
-        fm_mul(inv, inv, d);
-      } else {
-        ig = inv;
-      }
-      AffPt C = P;
-      if (jg != 0) {
-        if ((skip >> g) & 1u) ig = fe_small(0);
-        Fe s, x, y;
-        fm_sub(s, O.y, P.y);
-        fm_mul(s, s, ig);
-        fm_sqr(x, s);
-        fm_sub(x, x, P.x);
-        fm_sub(x, x, O.x);
-        fm_canon(x, x);
-        fm_sub(y, O.x, x);
-        fm_mul(y, y, s);
-        fm_sub(y, y, O.y);
-        fm_canon(y, y);
-        C.x = x;
-        C.y = y;
-      }
-      sr.stfe(SC + 2 * g, C.x);
-      sr.stfe(SC + 2 * g + 1, C.y);
-    }
-  }
-  // 1. forward passes (F9): prefixes of dx_i = GSn[i].x + (p - C.x)
-  const Fe g2x = gsn.x(kHalf);
-  uint32_t degen = 0;
-  F9 acc;
-  for (uint32_t g = 0; g < nb; ++g) {
-    const uint32_t e0 = g * kHalf;
-    const Fe cx = sr.ldfe(SC + 2 * g);
-    F9 ncx;
-    {
-      Fe p, t;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) p.v[k] = k == 0 ? KHB_P0 : (k == 1 ? KHB_P1 : 0xFFFFFFFFu);
-      fm_sub(t, p, cx);
-      f9_from_fe(ncx, t);
-    }
-    F9 a, dx;
-    f9_add(a, g9.x(0), ncx);
-    sr.st9(e0, a);
-    for (uint32_t i = 1; i < kHalf - 1; ++i) {
-      f9_add(dx, g9.x(i), ncx);
-      f9_mul(a, a, dx);
-      sr.st9(e0 + i, a);
-    }
-    f9_add(dx, g9.x(kHalf - 1), ncx);
-    f9_mul(a, a, dx);
-    Fe ac;
-    f9_to_fe(ac, a);
-    if (fe_is_zero(ac) || fe_eq(g2x, cx)) {
-      degen |= 1u << g;
-      a = f9_small(1);
-    }
-    sr.st9(e0 + kHalf - 1, a);
-    if (g == 0) acc = a; else f9_mul(acc, acc, a);
-    sr.st9(SQ + g, acc);
-  }
-  // 2. one inversion for the batch
-  F9 inv;
-  f9_inv(inv, acc);
-  for (int g = (int)nb - 1; g >= 0; --g) {
-    const uint32_t e0 = (uint32_t)g * kHalf;
-    F9 ig;
-    if (g > 0) {
-      f9_mul(ig, inv, sr.ld9(SQ + g - 1));
-      f9_mul(inv, inv, sr.ld9(e0 + kHalf - 1));
-    } else {
-      ig = inv;
-    }
-    if ((degen >> g) & 1u) ig = f9_small(0);
-    sr.st9(e0 + kHalf - 1, ig);
-  }
-  // 3. backward walks
-  uint32_t walked = 0;
-  for (uint32_t g = 0; g < nb; ++g, ++walked) {
-    const uint32_t e0 = g * kHalf;
-    asm volatile("" ::: "memory");
-    const AffPt C{sr.ldfe(SC + 2 * g), sr.ldfe(SC + 2 * g + 1)};
-    walk_group_g9<MODE>(A, Q, C, sr.ld9(e0 + kHalf - 1), job, g0 + g, sr, e0);
-    if (MODE != kDumpG && ((degen >> g) & 1u)) {
-      const uint32_t k = atomicAdd(&A.counters[1], 1u);
-      if (k < A.degen_cap) A.degen[k] = khb_degenerate{job, g0 + g};
-    }
-  }
-  return walked;
-}
 
 // Groups walked by the launch: a wave sum of every lane's count, one 64-bit atomic per wave into
 // counters[4..5].  The host compares it with n_jobs x group_count (khb_collect: KHB_EINCOMPLETE), so
@@ -1435,8 +879,22 @@ __device__ __forceinline__ void count_walked(uint32_t* counters, uint32_t walked
     atomicAdd(reinterpret_cast<unsigned long long*>(counters + 4), (unsigned long long)walked);
 }
 
+// Shader clock over the launch: the first wave of block 0 samples s_memtime (shader clock) and
+// s_memrealtime (100 MHz) when it starts and when it leaves (it takes work items until the launch's
+// queue is empty, so it spans the launch); the host turns the two deltas into MHz (khb_stats.shader_mhz).
+// The samples are stored with ordinary (vector) global stores by one lane.
+__device__ __forceinline__ void clock_probe(uint32_t* counters, int at) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint64_t t = __builtin_amdgcn_s_memtime(), r = __builtin_amdgcn_s_memrealtime();
+    uint64_t* c = reinterpret_cast<uint64_t*>(counters + 8) + 2 * at;
+    c[0] = t;
+    c[1] = r;
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kBlock, waves_per_simd(MODE)) void k_giant_scan(ScanArgs A) {
+  clock_probe(A.counters, 0);
   constexpr bool QUEUE = is_scan(MODE);
   constexpr bool BATCH = is_scan(MODE) || MODE == kDump || MODE == kDumpG;
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1446,16 +904,11 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(MODE)) void k_giant_scan(Sca
   // F9 walk: the group's p - C.x and C.y per lane in LDS (walk_group_g9), not in 18 VGPRs
   __shared__ uint32_t s_cn[is_f9(MODE) ? kWavesPerBlock : 1][is_f9(MODE) ? 18 * 64 : 1];
   const uint32_t wave = QUEUE ? threadIdx.x >> 6 : 0;
-#if KHB_LDSCOUNT
   ProbeQueue Q{s_queue[wave], (LdsWords)s_cn[is_f9(MODE) ? wave : 0],
                (volatile __attribute__((address_space(3))) uint32_t*)&s_count[wave]};
-#else
-  ProbeQueue Q{s_queue[wave], (LdsWords)s_cn[is_f9(MODE) ? wave : 0], &s_count[wave]};
-#endif
   if (QUEUE) *Q.n = 0;
   uint32_t walked = 0;     // groups this lane walked (count_walked: the host checks the launch's total)
   if constexpr (BATCH) {
-#if KHB_DYN
     // Dynamic work items: each wave takes the next 64 items from a launch-wide counter
     // (counters[2], zeroed per launch), so a wave that runs ahead keeps taking work and every SIMD
     // stays 4 waves deep until the queue is empty; a static lane-strided split left the launch's
@@ -1472,26 +925,15 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(MODE)) void k_giant_scan(Sca
         const uint32_t m = (uint32_t)(item % A.lanes_per_job);
         const uint32_t g0 = A.group_begin + m * kBatch;
         const uint32_t g1 = min(g0 + kBatch, A.group_end);
+#if KHB_F9WALK
         if constexpr (is_f9(MODE))
           walked += scan_batch9<MODE>(A, Q, job, g0, g1, lane);
         else
+#endif
           walked += scan_batch<MODE>(A, Q, job, g0, g1, scr);
       }
     }
-#else
-    for (uint64_t item = lane; item < A.n_items; item += A.stride) {
-      const uint32_t job = (uint32_t)(item / A.lanes_per_job);
-      const uint32_t m = (uint32_t)(item % A.lanes_per_job);
-      const uint32_t g0 = A.group_begin + m * kBatch;
-      const uint32_t g1 = min(g0 + kBatch, A.group_end);
-      if constexpr (is_f9(MODE))
-        walked += scan_batch9<MODE>(A, Q, job, g0, g1, lane);
-      else
-        walked += scan_batch<MODE>(A, Q, job, g0, g1, scr);
-    }
-#endif
   } else {
-#if KHB_DYN
     // dynamic per-wave items, as above (counters[2])
     const uint32_t wl = threadIdx.x & 63u;
     for (;;) {
@@ -1501,9 +943,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(MODE)) void k_giant_scan(Sca
       if (b >= A.n_items) break;
       const uint64_t item = (uint64_t)b + wl;
       if (item >= A.n_items) continue;
-#else
-    for (uint64_t item = lane; item < A.n_items; item += A.stride) {
-#endif
       const uint32_t job = (uint32_t)(item / A.lanes_per_job);
       const uint32_t m = (uint32_t)(item % A.lanes_per_job);
       const uint32_t g0 = A.group_begin + m * A.gpl;
@@ -1521,6 +960,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(MODE)) void k_giant_scan(Sca
   }
   if (QUEUE) q_drain(A, Q, 1);   // the wave has reconverged: finish what is still queued
   count_walked(A.counters, walked);
+  clock_probe(A.counters, 1);
 }
 
 // Launchers of the k_giant_scan instances (one translation unit each, see above).

@@ -33,7 +33,8 @@ class AddrHit(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("n_cand", C.c_uint32), ("n_degenerate", C.c_uint32), ("giant_steps", C.c_uint64),
-                ("kernel_ms", C.c_float), ("launch_begin_ms", C.c_double), ("launch_end_ms", C.c_double)]
+                ("kernel_ms", C.c_float), ("launch_begin_ms", C.c_double), ("launch_end_ms", C.c_double),
+                ("shader_mhz", C.c_float)]
 
 
 _libs: dict[str, C.CDLL] = {}

@@ -226,7 +226,8 @@ class Tables:
                      "kernel_s": stats[4] / 1e6, "launches": stats[5]}
 
 
-_STAT_KEYS = ("chunks", "giant_steps", "candidates", "degenerate", "kernel_s", "launches", "rescans", "busy_s")
+_STAT_KEYS = ("chunks", "giant_steps", "candidates", "degenerate", "kernel_s", "launches", "rescans", "busy_s",
+              "shader_mhz")
 
 
 class Session:
@@ -256,7 +257,7 @@ class Session:
         n = len(targets_xy)
         found = (C.c_int * n)()
         keys = C.create_string_buffer(32 * n)
-        stats = (C.c_uint64 * 8)()
+        stats = (C.c_uint64 * 9)()
         err = C.create_string_buffer(256)
         rc = lib().khh_session_run(self.h, b"".join(targets_xy), n, _b32(start), _b32(end), max_chunks,
                                    1 if random_chunks else 0, found, keys, stats, err, 256)
@@ -266,6 +267,7 @@ class Session:
         st = {k: int(stats[i]) for i, k in enumerate(_STAT_KEYS)}
         st["kernel_s"] = stats[4] / 1e6
         st["busy_s"] = stats[7] / 1e6
+        st["shader_mhz"] = stats[8] / 1e3
         return res, st
 
     def set_test_hooks(self, cand_cap: int = 0, use_gate: bool = True, record: bool = False,
@@ -356,7 +358,7 @@ class Addr:
         comp = C.create_string_buffer(cap)
         rmd = C.create_string_buffer(20 * cap)
         nf = C.c_uint32(0)
-        st = (C.c_uint64 * 6)()
+        st = (C.c_uint64 * 7)()
         devs = (C.c_int * len(devices))(*devices)
         err = C.create_string_buffer(256)
         rc = lib().khh_addr_search(self.h, _b32(start), _b32(end), search, 1 if random_chunks else 0, devs,
@@ -367,4 +369,4 @@ class Addr:
         found = [(int.from_bytes(keys.raw[32 * i:32 * i + 32], "big"), bool(comp.raw[i]), rmd.raw[20 * i:20 * i + 20])
                  for i in range(n)]
         return found, {"chunks": st[0], "keys": st[1], "hits": st[2], "degenerate": st[3], "kernel_s": st[4] / 1e6,
-                       "launches": st[5]}
+                       "launches": st[5], "shader_mhz": st[6] / 1e3}

@@ -7,6 +7,14 @@
 #include "device/hash160.hpp"
 using namespace khb;
 
+// hash160 of both compressed keys 02 || x and 03 || x in one scope: the two messages differ only in
+// word 0, so their SHA-256 schedules share W17, W19, W21 and the partial sums of words 18..30 (round-2
+// experiment KHB_ADDR_PAIR: 4401 VALU for the pair vs 2 x 2249, no faster in the kernel).
+__device__ __forceinline__ void hash160_compressed_pair(uint32_t out2[5], uint32_t out3[5], const Fe& x) {
+  hash160_compressed(out2, 2u, x);
+  hash160_compressed(out3, 3u, x);
+}
+
 __global__ void k_sha_block(const uint32_t* in, uint32_t* out) {       // one SHA-256 compression
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   uint32_t w[16], s[8];

@@ -22,7 +22,7 @@
 enum {
   ADD_U32, MOV_B32, AND_B32, LSHR_B32, ADD_CO_E32, ADDC_E32, ADDC_E32_NOP, ADD_CO_E64, ADDC_E64, MAD64, MAD64_VCC,
   MAD_ADDC_NOP, MAD_ADDC, MUL_LO, MUL_HI, MUL_U24, MULHI_U24, MAD_U24, ADD3, ALIGNBIT, LSHR_B64, LSHL_ADD_U64, CNDMASK,
-  BITOP3, BFE, LSHL_OR, AND_OR, PERM, SUB_CO_E32, NOP_ONLY, CND_VCMP, CND_E64, CMP_CND, N_OPS
+  BITOP3, BFE, LSHL_OR, AND_OR, PERM, SUB_CO_E32, NOP_ONLY, CND_VCMP, CND_E64, CMP_CND, MAD_ADDU, MAD_2ADDU, ADDC_ADDU, MAD_BANK_SAME, MAD_BANK_DIFF, MAD_BITOP3, N_OPS
 };
 static const char* kNames[N_OPS] = {
   "v_add_u32", "v_mov_b32", "v_and_b32", "v_lshrrev_b32", "v_add_co_u32_e32(vcc)", "v_addc_co_u32_e32(vcc chain)",
@@ -31,7 +31,8 @@ static const char* kNames[N_OPS] = {
   "v_mul_u32_u24", "v_mul_hi_u32_u24", "v_mad_u32_u24", "v_add3_u32", "v_alignbit_b32", "v_lshrrev_b64",
   "v_lshl_add_u64", "v_cndmask_b32(vcc)", "v_bitop3_b32", "v_bfe_u32", "v_lshl_or_b32", "v_and_or_b32", "v_perm_b32",
   "v_sub_co_u32_e32(vcc)", "s_nop 0 only", "v_cndmask_b32(vcc from v_cmp)", "v_cndmask_b32_e64(sgpr v_cmp)",
-  "v_cmp+v_cndmask pair"};
+  "v_cmp+v_cndmask pair", "mad + v_add_u32 pair", "mad + 2 v_add_u32", "addc(e64) + v_add_u32 pair",
+  "mad srcs same bank (fixed regs)", "mad srcs 4 banks (fixed regs)", "mad + v_bitop3 pair"};
 // instructions counted per body (pairs count 2; NOP_ONLY counts the nop)
 static int kPer[N_OPS];
 
@@ -75,6 +76,25 @@ __device__ __forceinline__ void body(uint32_t& x, uint64_t& y, uint64_t& sc, uin
   if constexpr (OP == NOP_ONLY) asm volatile("s_nop 0");
   if constexpr (OP == CND_VCMP) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(x) : "v"(b));
   if constexpr (OP == CND_E64) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(x) : "v"(b), "s"(sc));
+  if constexpr (OP == MAD_ADDU) {
+    uint64_t sg;
+    asm volatile("v_mad_u64_u32 %0, %2, %3, %4, %0\n\tv_add_u32 %1, %1, %3" : "+v"(y), "+v"(x), "=s"(sg) : "v"(b), "v"(c));
+  }
+  if constexpr (OP == MAD_2ADDU) {
+    uint64_t sg;
+    asm volatile("v_mad_u64_u32 %0, %2, %3, %4, %0\n\tv_add_u32 %1, %1, %3\n\tv_xor_b32 %1, %1, %4"
+                 : "+v"(y), "+v"(x), "=s"(sg) : "v"(b), "v"(c));
+  }
+  if constexpr (OP == ADDC_ADDU)
+    asm volatile("v_addc_co_u32_e64 %0, %2, %0, %3, %2\n\tv_add_u32 %1, %1, %3" : "+v"(x), "+v"(c), "+s"(sc) : "v"(b));
+  if constexpr (OP == MAD_BANK_SAME)
+    asm volatile("v_mad_u64_u32 v[40:41], s[40:41], v44, v48, v[40:41]" ::: "v40", "v41", "v44", "v48", "s40", "s41");
+  if constexpr (OP == MAD_BANK_DIFF)
+    asm volatile("v_mad_u64_u32 v[40:41], s[40:41], v45, v46, v[40:41]" ::: "v40", "v41", "v45", "v46", "s40", "s41");
+  if constexpr (OP == MAD_BITOP3) {
+    uint64_t sg;
+    asm volatile("v_mad_u64_u32 %0, %2, %3, %4, %0\n\tv_bitop3_b32 %1, %1, %3, %4 bitop3:0x96" : "+v"(y), "+v"(x), "=s"(sg) : "v"(b), "v"(c));
+  }
   if constexpr (OP == CMP_CND)
     asm volatile("v_cmp_gt_u32_e32 vcc, %0, %1\n\ts_nop 1\n\tv_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(x) : "v"(b) : "vcc");
 }
@@ -164,5 +184,7 @@ int main() {
   row<BITOP3>(d, clk, cus, 1); row<BFE>(d, clk, cus, 1); row<LSHL_OR>(d, clk, cus, 1);
   row<AND_OR>(d, clk, cus, 1); row<PERM>(d, clk, cus, 1); row<NOP_ONLY>(d, clk, cus, 1);
   row<CND_VCMP>(d, clk, cus, 1); row<CND_E64>(d, clk, cus, 1); row<CMP_CND>(d, clk, cus, 2);
+  row<MAD_ADDU>(d, clk, cus, 2); row<MAD_2ADDU>(d, clk, cus, 3); row<ADDC_ADDU>(d, clk, cus, 2);
+  row<MAD_BANK_SAME>(d, clk, cus, 1); row<MAD_BANK_DIFF>(d, clk, cus, 1); row<MAD_BITOP3>(d, clk, cus, 2);
   return 0;
 }

@@ -5,7 +5,10 @@ per launch.
 GATE=0|1|both (default both): run every library without / with the level-0 gate.
 GATE_LOG2S=23,24 adds gates of those sizes, folded from the tables' gate (64-bit block i of a
 2^(L-1)-bit map is block i | block i + 2^(L-7) of the 2^L map: the same map a 2^(L-1) build writes,
-the block index being (x mod 2^32) mod 2^(L-6))."""
+the block index being (x mod 2^32) mod 2^(L-6)).
+GATE_ZERO=L adds an all-zero gate of 2^L bits (L >= 13): the same gate code and instructions, but every
+block load hits the vector L1 (1 KiB at L = 13) and no x passes, which isolates the cost of the real
+gate's cache misses (verdict r2 item 4); its candidate set is empty by construction."""
 import glob
 import os
 import statistics
@@ -35,30 +38,39 @@ for lg in [int(v) for v in os.environ.get("GATE_LOG2S", "").split(",") if v]:
     blocks = np.frombuffer(gate, np.uint64)
     gates[lg] = np.bitwise_or.reduce(blocks.reshape(1 << (glog - lg), -1), axis=0).tobytes()
     gsets.append(lg)
+if int(os.environ.get("GATE_ZERO", "0") or 0):
+    lz = int(os.environ["GATE_ZERO"])
+    gates[-lz] = bytes((1 << lz) // 8)
+    gsets.append(-lz)
 engines = {}
 for p in paths:
     for g in gsets:
         e = Engine(0, lib_path=p)
         e.load_bloom(bf, nb, bits, h)
         if g:
-            e.load_gate(gates[g], g, t.gate_probes())
+            e.load_gate(gates[g], abs(g), t.gate_probes())
         e.load_giant_table(gsn)
         e.load_lane_offsets(offs, gpl)
         e.scan(centres[:64 * 8], 0, 64)
-        name = os.path.basename(p) + (f" +gate{g}" if g else "")
+        name = os.path.basename(p) + (f" +gate{g}" if g > 0 else f" +zerogate{-g}" if g else "")
         engines[name] = (e, g)
         print(f"{name}: lanes {e.lanes()}", flush=True)
 times = {n: [] for n in engines}
+mhz = {n: [] for n in engines}
 ncand = {}
 ref = {}
 for rnd in range(int(os.environ.get("ROUNDS", "3"))):
     for n, (e, g) in engines.items():
         c, d, st = e.scan(centres, 0, t.cycles)
         times[n].append(st.kernel_ms)
+        mhz[n].append(getattr(st, "shader_mhz", 0.0))
         ncand[n] = len(c)
         if "_p" in n.split()[0] or "nonop" in n:   # probe / timing-only experiments: not comparable
             continue
         s = sorted(c)
+        if g < 0:                                  # the zero gate: nothing passes
+            assert not s, f"{n}: a zero gate passed candidates"
+            continue
         ref.setdefault(g, s)
         assert s == ref[g], f"{n}: candidate set differs"
 for g in ref:   # a gate keeps a subset of the L1 candidates
@@ -67,4 +79,4 @@ steps = jobs * t.cycles * 1024
 for n in engines:
     med = statistics.median(times[n])
     print(f"{n:34s} median {med:8.2f} ms  min {min(times[n]):8.2f}  {steps / med / 1e6:8.3f} G steps/s"
-          f"  cand {ncand[n]}", flush=True)
+          f"  cand {ncand[n]}  clock {statistics.median(mhz[n]):7.1f} MHz", flush=True)
