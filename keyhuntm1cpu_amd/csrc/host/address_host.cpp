@@ -425,7 +425,9 @@ void device_loop(AddrShared& S, int device) {
     khb_stats st{};
     const int crc = khb_addr_collect(ctx, hits.data(), (uint32_t)hits.size(), &st);
     if (crc) { fail(crc, "khb_addr_collect"); rc = crc; continue; }   // keep draining the queue
-    if (pre >= 0 && !rc) {
+    // after a stop (every target found, or the caller's stop) the prepared batch is dropped instead of
+    // queued, so the exit waits for at most the one launch still in flight (advisor r2)
+    if (pre >= 0 && !rc && !(S.cb.stop && S.cb.stop())) {
       if ((rc = submit(ring[pre]))) fail(rc, "khb_addr_submit");
       else q.push_back(pre);
     }
