@@ -65,7 +65,7 @@ for rnd in range(int(os.environ.get("ROUNDS", "3"))):
         times[n].append(st.kernel_ms)
         mhz[n].append(getattr(st, "shader_mhz", 0.0))
         ncand[n] = len(c)
-        if "_p" in n.split()[0] or "nonop" in n:   # probe / timing-only experiments: not comparable
+        if "_p" in n.split()[0] or "nonop" in n or "_rm" in n or "_scr" in n:   # timing-only experiments: not comparable
             continue
         s = sorted(c)
         if g < 0:                                  # the zero gate: nothing passes
