@@ -33,7 +33,10 @@ struct AffPt {
 #define KHB_GATE1 25              // default log2 bytes of the stage-1 fold of a larger level-0 gate (0 = none)
 #endif
 #ifndef KHB_WAVES_PER_SIMD
-#define KHB_WAVES_PER_SIMD 4      // occupancy target of k_giant_scan (launch bounds); w4 measured best
+// occupancy target of k_giant_scan (launch bounds).  Round 3: 3 waves/SIMD (168 VGPRs, 196,608 lanes)
+// ran 1.4-1.6 % faster than 4 (128 VGPRs) in two A/B runs, 2 waves 6 % slower
+// (profiles/r03_calibration/occupancy_ab*.txt); round 1 had measured 3 and 4 equal.
+#define KHB_WAVES_PER_SIMD 3
 #endif
 constexpr uint32_t kBlock = 256;
 #ifndef KHB_BATCH

@@ -6,8 +6,10 @@
 #                 8 s_nop, 9 v_add3) in 4 independent chains; KHB_PAD_OP=0 is the barrier-only control.
 #   rm_patch.py:  KHB_RM_FOLD / KHB_RM_T / KHB_RM_P replace existing carry chains or mads by
 #                 full-rate ops (results wrong by design; perf_variants skips the parity check for _rm*).
+#   pair_patch.py: the paired reduction (exact; slower at 4 waves because it spills).
+#   defer_patch.py: the gate tested one walk step after its loads, pending x pair in registers.
 #   scr_patch.py: KHB_SCR_MASK=m keeps the prefix scratch in (i & m) entries per group (no HBM stream).
-# Usage: tools/experiments/calib_build.sh pad|rm|scr <name> [-DKEY=VAL ...]
+# Usage: tools/experiments/calib_build.sh pad|rm|scr|pair|defer <name> [-DKEY=VAL ...]
 set -e
 KIND=$1; NAME=$2; shift 2
 S1=keyhuntm1cpu_amd/csrc/device/fe_asm.hpp

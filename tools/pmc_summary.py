@@ -1,65 +1,79 @@
-"""Summarise rocprofv3 outputs of tools/profile_bench.sh for k_giant_scan.
-Usage: python tools/pmc_summary.py gpurun_out/<tag> [--write-latest]
-Writes profiles/pmc_latest.json with --write-latest (read by bench.py for roofline.traffic)."""
+"""profiles/pmc_latest.json from the PMC passes of tools/gpu/r03u.sh (bench.py reads it for
+roofline.traffic and the executed VALU figures).
+
+Inputs (rocprofv3 --pmc CSVs, one timed k_giant_scan launch each, JOBS chunks of the default k=1
+geometry; the tiny first dispatch of perf_variants is skipped):
+  pmc_fetch_0   FETCH_SIZE, TCC_EA0_RDREQ_sum with the real 2^28-bit gate
+  pmc_fetch_13  the same launches plus the all-zero 1 KiB gate's (no gate traffic)
+  pmc_write_0   WRITE_SIZE, TCC_EA0_WRREQ_sum
+  pmc_sq        SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE, ...
+Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half of a wide coalesced
+streaming read, so the prefix stream's read bytes are 2 x the zero-gate launch's FETCH_SIZE;
+WRITE_SIZE is exact for the 16-B-per-lane prefix stores.  The gate's reads are the extra memory-side
+read requests of the real-gate launch (TCC_EA0_RDREQ real - zero) x 64 B (FETCH_SIZE = RDREQ x 64 B;
+the scattered 8-B probe's request width is not calibrated, and Infinity-Cache hits are counted with
+HBM reads: these are memory-side bytes, HBM or MALL).
+Usage: python tools/pmc_summary.py <dir with the pmc_* subdirs> <chunks per launch> [out.json]"""
+import collections
 import csv
 import json
 import os
-import statistics
 import sys
-from collections import defaultdict
 
-d = sys.argv[1]
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GROUPS = 4096          # k=1 default geometry: groups per chunk (cycles)
 
 
-def per_dispatch(path, counter):
-    agg = defaultdict(float)
-    for r in csv.DictReader(open(path)):
-        if "k_giant_scan" in r["Kernel_Name"] and r["Counter_Name"] == counter:
-            agg[int(r["Dispatch_Id"])] += float(r["Counter_Value"])
-    return agg
+def dispatches(d):
+    out = collections.defaultdict(dict)
+    with open(os.path.join(d, "pmc_counter_collection.csv"), newline="") as f:
+        for r in csv.DictReader(f):
+            if "k_giant_scan" in r["Kernel_Name"]:
+                out[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
+    return [out[k] for k in sorted(out)]
 
 
-fetch = per_dispatch(os.path.join(d, "fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
-write = per_dispatch(os.path.join(d, "write", "write_counter_collection.csv"), "WRITE_SIZE")
-bench = json.load(open(os.path.join(d, "bench.json")))
-chunks = bench["config"]["chunks_per_step"]
-steps_per_launch = bench["config"]["giant_steps_per_step"]
-# the largest dispatches are the full-size launches (warmup + timed); small ones are partial
-fmax = max(fetch.values())
-f_full = [v for v in fetch.values() if v > 0.9 * fmax]
-w_full = sorted(write.values())[-len(f_full):]
-f_kib, w_kib = statistics.mean(f_full), statistics.mean(w_full)
-valu_path = os.path.join(d, "valu", "valu_counter_collection.csv")
-valu = {}
-if os.path.exists(valu_path):
-    for cn in ("SQ_INSTS_VALU", "VALUBusy", "OccupancyPercent"):
-        v = per_dispatch(valu_path, cn)
-        vmax = max(v.values()) if v else 0
-        full = [x for x in v.values() if x > 0.9 * vmax] if cn == "SQ_INSTS_VALU" else list(v.values())
-        valu[cn] = statistics.mean(full) if full else None
-stats = list(csv.DictReader(open(os.path.join(d, "trace", "trace_kernel_stats.csv"))))
-scan = [r for r in stats if "k_giant_scan" in r["Name"]]
-out = {
-    "kernel": "k_giant_scan",
-    "k": int(bench["config"]["workload"].split("-k ")[1].split()[0]),
-    "chunks_per_launch": chunks,
-    "giant_steps_per_launch": steps_per_launch,
-    "dispatches_averaged": len(f_full),
-    "fetch_size_kib": f_kib,
-    "write_size_kib": w_kib,
-    "hbm_bytes_per_launch": int((f_kib + w_kib) * 1024),
-    "bytes_per_giant_step": round((f_kib + w_kib) * 1024 / steps_per_launch, 2),
-    "trace_avg_ns": float(scan[0]["AverageNs"]) if scan else None,
-    "valu_instr_per_giant_step": round(valu["SQ_INSTS_VALU"] * 64 / steps_per_launch, 1) if valu.get("SQ_INSTS_VALU") else None,
-    "valu_busy_pct": round(valu["VALUBusy"], 2) if valu.get("VALUBusy") else None,
-    "occupancy_pct": round(valu["OccupancyPercent"], 2) if valu.get("OccupancyPercent") else None,
-    "valu_source": os.path.relpath(valu_path, REPO) if valu else None,
-    "note": "FETCH_SIZE+WRITE_SIZE (KiB) x 1024 per full-size dispatch, uncorrected: the access mix "
-            "(1-B random bloom probes, 16-B scratch streams, LDS-free spills) has no gfx950 calibration, and "
-            "FETCH_SIZE counts Infinity-Cache hits (MI355X_MICROARCH.md HBM section)",
-    "source": os.path.relpath(d, REPO),
-}
-print(json.dumps(out, indent=1))
-if "--write-latest" in sys.argv:
-    json.dump(out, open(os.path.join(REPO, "profiles", "pmc_latest.json"), "w"), indent=1)
+def main():
+    src, chunks = sys.argv[1], int(sys.argv[2])
+    dst = sys.argv[3] if len(sys.argv) > 3 else os.path.join(REPO, "profiles", "pmc_latest.json")
+    steps = chunks * GROUPS * 1024
+    real_f = dispatches(os.path.join(src, "pmc_fetch_0"))[-1]
+    both_f = dispatches(os.path.join(src, "pmc_fetch_13"))
+    zero_f = both_f[-1]                    # the zero gate runs after the real one in perf_variants
+    real_w = dispatches(os.path.join(src, "pmc_write_0"))[-1]
+    sq = dispatches(os.path.join(src, "pmc_sq"))[-1]
+    stream_rd = 2 * zero_f["FETCH_SIZE"] * 1024
+    stream_wr = real_w["WRITE_SIZE"] * 1024
+    gate_rd = (real_f["TCC_EA0_RDREQ_sum"] - zero_f["TCC_EA0_RDREQ_sum"]) * 64
+    xcds = 8
+    out = {
+        "kernel": "k_giant_scan", "k": 1, "chunks_per_launch": chunks, "giant_steps_per_launch": steps,
+        "fetch_size_kib_real_gate": real_f["FETCH_SIZE"], "fetch_size_kib_zero_gate": zero_f["FETCH_SIZE"],
+        "write_size_kib": real_w["WRITE_SIZE"],
+        "ea_rdreq_real_gate": real_f["TCC_EA0_RDREQ_sum"], "ea_rdreq_zero_gate": zero_f["TCC_EA0_RDREQ_sum"],
+        "ea_wrreq": real_w["TCC_EA0_WRREQ_sum"],
+        "prefix_stream_read_bytes_per_giant_step": round(stream_rd / steps, 2),
+        "prefix_stream_write_bytes_per_giant_step": round(stream_wr / steps, 2),
+        "gate_read_requests_per_giant_step": round(gate_rd / 64 / steps, 4),
+        "gate_read_bytes_per_giant_step": round(gate_rd / steps, 2),
+        "hbm_bytes_per_launch": int(stream_rd + stream_wr + gate_rd),
+        "bytes_per_giant_step": round((stream_rd + stream_wr + gate_rd) / steps, 2),
+        "algorithmic_bytes_per_giant_step": 40,
+        "valu_instr_per_giant_step": round(sq["SQ_INSTS_VALU"] * 64 / steps, 1),
+        "valu_busy_pct": round(100 * sq["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / (sq["GRBM_GUI_ACTIVE"] / xcds), 2),
+        "valu_source": os.path.relpath(os.path.join(src, "pmc_sq"), REPO),
+        "note": "traffic = prefix-stream reads (2 x FETCH_SIZE of the zero-gate launch, the gfx950 streaming-read "
+                "correction) + prefix-stream writes (WRITE_SIZE) + the gate's extra memory-side read requests x 64 B; "
+                "algorithmic = 16 B written + 16 B read of prefix scratch + one 8-B gate probe per giant step. "
+                "The gate's lines are fetched whole (64 B per 8-B probe); the counters do not separate "
+                "Infinity-Cache hits from HBM. VALUBusy = ACTIVE_INST_VALU x 4 / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 XCDs).",
+        "source": os.path.relpath(src, REPO),
+    }
+    with open(dst, "w") as f:
+        json.dump(out, f, indent=1)
+        f.write("\n")
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
