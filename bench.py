@@ -3,8 +3,9 @@
 
 --workload p66 (default; BASELINE.json configs[1], -b 66, k=1; --k 4 = configs[2]):
   one step = one GPU scan batch of the product search (libkhhost -> libkhbsgs): host centres for
-  4096 chunks, the HIP giant-step kernel over all 4096 groups of each chunk (2^34 giant steps: eight
-  8-group work items per lane of a full residency, as the CLI's auto batch), and the CPU confirmation
+  3072 chunks, the HIP giant-step kernel over all 4096 groups of each chunk (1.5 x 2^33 giant steps:
+  eight 8-group work items per lane of a full residency of 196,608 lanes at 3 waves/SIMD, as the CLI's
+  auto batch), and the CPU confirmation
   of every candidate, pipelined exactly as the keyhunt_amd CLI runs it.  The -b 66 range [2^65, 2^66)
   is partitioned statically into one contiguous chunk block per rank (partition.key_block, north_star);
   the block holding puzzle #66's (public) key starts at the chunk after the key's, so the search never
@@ -169,7 +170,7 @@ def main():
     t_build = time.time() - t0
     if not args.chunks:
         # eight work items per lane, as the CLI's auto batch (engine.cpp batch_chunks): waves take
-        # items dynamically (KHB_DYN), so a deeper queue keeps every SIMD 4 waves deep until the
+        # items dynamically (KHB_DYN), so a deeper queue keeps every SIMD 3 waves deep until the
         # launch's last items (profiles/r01c_dyn_probe.txt)
         from keyhuntm1cpu_amd import khbsgs
         fill = -(-khbsgs.default_lanes(local) * khbsgs.groups_per_item() // tables.cycles)

@@ -60,7 +60,8 @@ P66_KEY = 0x2832ED74F2B5E35EE        # puzzle #66's public solution (tests/66.rm
 def test_p66_static_blocks(world):
     """bench.py --workload p66 for N ranks: -b 66 split into N static blocks (keyhunt.cpp:508-527 sets
     the -b range, north_star partitions it); the key's block starts at the chunk after the key's; the
-    driver's 5 warmup + 20 timed steps of 4096 chunks (k = 1, 2N = 2^45) fit inside every block."""
+    driver's 5 warmup + 20 timed steps fit inside every block: checked at 4096 chunks per step (the
+    4-wave build's batch, k = 1, 2N = 2^45), so the 3-wave product's 3072 fit as well."""
     from keyhuntm1cpu_amd.partition import blocks_fit, key_block
     chunks = (5 + 20) * 4096
     blocks = blocks_fit(LO, HI, TWO_N, world, chunks, P66_KEY)

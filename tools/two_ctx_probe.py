@@ -14,7 +14,8 @@ t = khhost.Tables(None, int(os.environ.get("K", "1")), threads=16, gpl=4)
 tgt = khhost.pubkey(0x2832ED74F2B5E35EE)
 two_n = 2 * t.n_low
 lo = (1 << 65) + 4 * two_n
-R = 262144   # one full residency (lanes)
+from keyhuntm1cpu_amd import khbsgs  # noqa: E402
+R = khbsgs.default_lanes(0)   # one full residency (lanes)
 for nctx, lanes, cpb in ((1, 0, 1024), (1, 0, 4096), (1, 4 * R, 4096), (2, 0, 1024), (1, 0, 1024), (1, 0, 4096)):
     s = khhost.Session(t, devices=[0] * nctx, lanes=lanes, chunks_per_batch=cpb, check_threads=16)
     s.run([tgt], lo, lo + 4096 * two_n, max_chunks=2048)          # warm-up
