@@ -195,84 +195,53 @@ FM_DEV void fm_sqr512x(uint32_t t[16], const uint32_t* a) {
   uint64_t D[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) D[i] = (uint64_t)a[i] * a[i];
-  // t = D + c + c
+  // t = D + 2c: the doubled cross sum by one funnel shift per word (v_alignbit_b32, no carry flag:
+  // (c_k << 1) | (c_k-1 >> 31); c[0] = 0, and 2c < 2^512 since a^2 < 2^512), then one carry chain
+  // instead of adding c twice.
+  uint32_t c2[16];
+  c2[0] = 0u;
+  c2[1] = c[1] << 1;
+#pragma unroll
+  for (int k = 2; k < 16; ++k) c2[k] = __builtin_amdgcn_alignbit(c[k], c[k - 1], 31);
   uint32_t u[16];
-  asm("v_add_co_u32_e32 %0, vcc, %16, %32\n\t"
+  u[0] = (uint32_t)D[0];
+  asm("v_add_co_u32_e32 %0, vcc, %15, %30\n\t"
       KHB_NOP
-      "v_addc_co_u32_e32 %1, vcc, %17, %33, vcc\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %16, %31, vcc\n\t"
       KHB_NOP
-      "v_addc_co_u32_e32 %2, vcc, %18, %34, vcc\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %17, %32, vcc\n\t"
       KHB_NOP
-      "v_addc_co_u32_e32 %3, vcc, %19, %35, vcc\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %18, %33, vcc\n\t"
       KHB_NOP
-      "v_addc_co_u32_e32 %4, vcc, %20, %36, vcc\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %19, %34, vcc\n\t"
       KHB_NOP
-      "v_addc_co_u32_e32 %5, vcc, %21, %37, vcc\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %20, %35, vcc\n\t"
       KHB_NOP
-      "v_addc_co_u32_e32 %6, vcc, %22, %38, vcc\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %21, %36, vcc\n\t"
       KHB_NOP
-      "v_addc_co_u32_e32 %7, vcc, %23, %39, vcc\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %22, %37, vcc\n\t"
       KHB_NOP
-      "v_addc_co_u32_e32 %8, vcc, %24, %40, vcc\n\t"
+      "v_addc_co_u32_e32 %8, vcc, %23, %38, vcc\n\t"
       KHB_NOP
-      "v_addc_co_u32_e32 %9, vcc, %25, %41, vcc\n\t"
+      "v_addc_co_u32_e32 %9, vcc, %24, %39, vcc\n\t"
       KHB_NOP
-      "v_addc_co_u32_e32 %10, vcc, %26, %42, vcc\n\t"
+      "v_addc_co_u32_e32 %10, vcc, %25, %40, vcc\n\t"
       KHB_NOP
-      "v_addc_co_u32_e32 %11, vcc, %27, %43, vcc\n\t"
+      "v_addc_co_u32_e32 %11, vcc, %26, %41, vcc\n\t"
       KHB_NOP
-      "v_addc_co_u32_e32 %12, vcc, %28, %44, vcc\n\t"
+      "v_addc_co_u32_e32 %12, vcc, %27, %42, vcc\n\t"
       KHB_NOP
-      "v_addc_co_u32_e32 %13, vcc, %29, %45, vcc\n\t"
+      "v_addc_co_u32_e32 %13, vcc, %28, %43, vcc\n\t"
       KHB_NOP
-      "v_addc_co_u32_e32 %14, vcc, %30, %46, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %15, vcc, %31, %47, vcc"
-      : "=&v"(u[0]), "=&v"(u[1]), "=&v"(u[2]), "=&v"(u[3]), "=&v"(u[4]), "=&v"(u[5]), "=&v"(u[6]), "=&v"(u[7]),
-        "=&v"(u[8]), "=&v"(u[9]), "=&v"(u[10]), "=&v"(u[11]), "=&v"(u[12]), "=&v"(u[13]), "=&v"(u[14]),
-        "=&v"(u[15])
-      : "v"((uint32_t)D[0]), "v"((uint32_t)(D[0] >> 32)), "v"((uint32_t)D[1]), "v"((uint32_t)(D[1] >> 32)),
+      "v_addc_co_u32_e32 %14, vcc, %29, %44, vcc"
+      : "=&v"(u[1]), "=&v"(u[2]), "=&v"(u[3]), "=&v"(u[4]), "=&v"(u[5]), "=&v"(u[6]), "=&v"(u[7]), "=&v"(u[8]),
+        "=&v"(u[9]), "=&v"(u[10]), "=&v"(u[11]), "=&v"(u[12]), "=&v"(u[13]), "=&v"(u[14]), "=&v"(u[15])
+      : "v"((uint32_t)(D[0] >> 32)), "v"((uint32_t)D[1]), "v"((uint32_t)(D[1] >> 32)),
         "v"((uint32_t)D[2]), "v"((uint32_t)(D[2] >> 32)), "v"((uint32_t)D[3]), "v"((uint32_t)(D[3] >> 32)),
         "v"((uint32_t)D[4]), "v"((uint32_t)(D[4] >> 32)), "v"((uint32_t)D[5]), "v"((uint32_t)(D[5] >> 32)),
         "v"((uint32_t)D[6]), "v"((uint32_t)(D[6] >> 32)), "v"((uint32_t)D[7]), "v"((uint32_t)(D[7] >> 32)),
-        "v"(0u), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]), "v"(c[8]), "v"(c[9]),
-        "v"(c[10]), "v"(c[11]), "v"(c[12]), "v"(c[13]), "v"(c[14]), "v"(c[15])
-      : "vcc");
-  asm("v_add_co_u32_e32 %0, vcc, %0, %16\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %1, vcc, %1, %17, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %2, vcc, %2, %18, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %3, vcc, %3, %19, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %4, vcc, %4, %20, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %5, vcc, %5, %21, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %6, vcc, %6, %22, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %7, vcc, %7, %23, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %8, vcc, %8, %24, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %9, vcc, %9, %25, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %10, vcc, %10, %26, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %11, vcc, %11, %27, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %12, vcc, %12, %28, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %13, vcc, %13, %29, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %14, vcc, %14, %30, vcc\n\t"
-      KHB_NOP
-      "v_addc_co_u32_e32 %15, vcc, %15, %31, vcc"
-      : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]),
-        "+v"(u[8]), "+v"(u[9]), "+v"(u[10]), "+v"(u[11]), "+v"(u[12]), "+v"(u[13]), "+v"(u[14]), "+v"(u[15])
-      : "v"(0u), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]), "v"(c[8]), "v"(c[9]),
-        "v"(c[10]), "v"(c[11]), "v"(c[12]), "v"(c[13]), "v"(c[14]), "v"(c[15])
+        "v"(c2[1]), "v"(c2[2]), "v"(c2[3]), "v"(c2[4]), "v"(c2[5]), "v"(c2[6]), "v"(c2[7]), "v"(c2[8]),
+        "v"(c2[9]), "v"(c2[10]), "v"(c2[11]), "v"(c2[12]), "v"(c2[13]), "v"(c2[14]), "v"(c2[15])
       : "vcc");
 #pragma unroll
   for (int i = 0; i < 16; ++i) t[i] = u[i];
