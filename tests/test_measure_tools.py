@@ -1,0 +1,112 @@
+"""CPU: the measurement tools behind bench.py's roofline.
+
+tools/trace_union.py turns a rocprofv3 kernel trace into device-busy time per step (the union of
+overlapping launch intervals, which bench.py computes from HIP events); tools/pmc_summary.py turns the
+real-gate / zero-gate PMC passes into profiles/pmc_latest.json's corrected traffic.  Both are checked
+on synthetic inputs with known answers, and the committed pmc_latest.json against its own raw CSVs.
+"""
+from __future__ import annotations
+
+import csv
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+import pmc_summary  # noqa: E402
+import trace_union  # noqa: E402
+
+
+def test_union_of_overlapping_launches():
+    # two slots: each launch overlaps the next; gaps are not busy time
+    iv = [(0, 10), (8, 20), (18, 30), (40, 50), (45, 47)]
+    assert trace_union.union_ns(iv) == 30 + 10
+    assert trace_union.union_ns([]) == 0
+    assert trace_union.union_ns([(5, 5)]) == 0
+    assert trace_union.union_ns([(0, 4), (4, 9)]) == 9
+
+
+def _trace(path, rows):
+    with open(path, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        w.writeheader()
+        for name, s, e in rows:
+            w.writerow({"Kernel_Name": name, "Start_Timestamp": s, "End_Timestamp": e})
+
+
+def test_trace_union_cli_uses_the_last_launches(tmp_path):
+    # 2 warmup + 3 timed launches of k_giant_scan (ms in ns), plus another kernel that must be ignored
+    ms = 1_000_000
+    rows = [("void khbk::k_giant_scan<7>(khbk::ScanArgs)", s * ms, e * ms)
+            for s, e in ((0, 100), (90, 190), (180, 280), (270, 370), (360, 460))]
+    rows.append(("k_expand_offsets", 0, 10 * ms))
+    tr = tmp_path / "trace.csv"
+    _trace(tr, rows)
+    bench = tmp_path / "bench.json"
+    bench.write_text(json.dumps({"ms_per_step": 93.5, "roofline": {"kernel_busy_ms_per_step": 93.3,
+                                                                   "kernel_ms_avg": 100.0}}) + "\n")
+    out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "trace_union.py"), str(tr), "--steps", "3",
+                          "--bench", str(bench)], capture_output=True, text=True, check=True)
+    d = json.loads(out.stdout)
+    assert d["launches_in_trace"] == 5 and d["launches_used"] == 3
+    assert d["launch_ms_avg"] == 100.0
+    assert d["busy_ms_per_step"] == round((460 - 180) / 3, 3)      # union of [180,280]+[270,370]+[360,460]
+    assert d["trace_over_bench_busy"] == round(d["busy_ms_per_step"] / 93.3, 4)
+
+
+def _pmc(d, dispatches):
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "pmc_counter_collection.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for did, counters in dispatches:
+            for k, v in counters.items():
+                w.writerow({"Dispatch_Id": did, "Kernel_Name": "void khbk::k_giant_scan<7>(khbk::ScanArgs)",
+                            "Counter_Name": k, "Counter_Value": v})
+
+
+def test_pmc_summary_corrections(tmp_path):
+    chunks = 2
+    steps = chunks * 4096 * 1024
+    # zero gate: the prefix stream only (16 B read per step, counted at half by FETCH_SIZE; 16 B
+    # written); real gate: + one 64-B request per step
+    rd_zero = steps * 16 / 128                 # 128-B requests, tallied as 64 B each
+    fetch_zero_kib = rd_zero * 64 / 1024
+    rd_real = rd_zero + steps
+    _pmc(tmp_path / "pmc_fetch_0", [(4, {"FETCH_SIZE": 1.0, "TCC_EA0_RDREQ_sum": 16.0}),
+                                    (7, {"FETCH_SIZE": rd_real * 64 / 1024, "TCC_EA0_RDREQ_sum": rd_real})])
+    _pmc(tmp_path / "pmc_fetch_13", [(4, {"FETCH_SIZE": 1.0, "TCC_EA0_RDREQ_sum": 16.0}),
+                                     (7, {"FETCH_SIZE": rd_real * 64 / 1024, "TCC_EA0_RDREQ_sum": rd_real}),
+                                     (9, {"FETCH_SIZE": fetch_zero_kib, "TCC_EA0_RDREQ_sum": rd_zero})])
+    _pmc(tmp_path / "pmc_write_0", [(7, {"WRITE_SIZE": steps * 16 / 1024, "TCC_EA0_WRREQ_sum": steps / 4})])
+    _pmc(tmp_path / "pmc_sq", [(7, {"SQ_INSTS_VALU": steps * 700 / 64, "SQ_ACTIVE_INST_VALU": steps * 700 / 64,
+                                    "GRBM_GUI_ACTIVE": 8.0 * steps * 700 / 64 * 4 / 1024})])
+    out = tmp_path / "pmc.json"
+    subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"), str(tmp_path), str(chunks),
+                    str(out)], capture_output=True, text=True, check=True)
+    d = json.loads(out.read_text())
+    assert d["prefix_stream_read_bytes_per_giant_step"] == 16.0
+    assert d["prefix_stream_write_bytes_per_giant_step"] == 16.0
+    assert d["gate_read_requests_per_giant_step"] == 1.0
+    assert d["bytes_per_giant_step"] == 96.0
+    assert d["hbm_bytes_per_launch"] == 96 * steps
+    assert d["valu_instr_per_giant_step"] == 700.0
+    assert d["valu_busy_pct"] == 100.0
+
+
+def test_committed_pmc_latest_reproduces_from_its_csvs(tmp_path):
+    """profiles/pmc_latest.json (bench.py's roofline.traffic) equals a rerun of the summary on the raw
+    CSVs it names."""
+    with open(os.path.join(REPO, "profiles", "pmc_latest.json")) as f:
+        cur = json.load(f)
+    out = tmp_path / "again.json"
+    subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"), os.path.join(REPO, cur["source"]),
+                    str(cur["chunks_per_launch"]), str(out)], capture_output=True, text=True, check=True)
+    again = json.loads(out.read_text())
+    for k in ("hbm_bytes_per_launch", "bytes_per_giant_step", "gate_read_requests_per_giant_step",
+              "valu_instr_per_giant_step"):
+        assert again[k] == cur[k], k
+    assert pmc_summary.GROUPS == 4096
