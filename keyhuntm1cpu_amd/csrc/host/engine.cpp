@@ -95,23 +95,25 @@ bool split_batch(const Batch& b, uint32_t cycles, uint32_t gpl, Batch& lo, Batch
   return true;
 }
 
-// Length of the union of [begin, end) intervals (ms).
-double union_ms(std::vector<std::pair<double, double>>& iv) {
-  std::sort(iv.begin(), iv.end());
-  double tot = 0, b = 0, e = -1;
-  for (const auto& x : iv) {
-    if (x.first < 0 || x.second < x.first) continue;
-    if (x.first > e) {
-      if (e > b) tot += e - b;
-      b = x.first;
-      e = x.second;
-    } else if (x.second > e) {
-      e = x.second;
+// Device-busy time of one context's launches: the length of the union of their [begin, end) intervals
+// (ms on the context's epoch).  Launches are collected in submission order and at most two overlap, so
+// intervals are merged as they arrive and only the open one is kept (a long CLI run stays O(1)); an
+// interval that starts before the open one (never seen) is merged into it.
+struct BusyUnion {
+  double total = 0, b = 0, e = -1;
+  void add(double lo, double hi) {
+    if (lo < 0 || hi < lo) return;                  // no timing for this launch
+    if (lo > e) {
+      if (e > b) total += e - b;
+      b = lo;
+      e = hi;
+    } else {
+      b = std::min(b, lo);
+      e = std::max(e, hi);
     }
   }
-  if (e > b) tot += e - b;
-  return tot;
-}
+  double ms() const { return total + (e > b ? e - b : 0); }
+};
 
 bool claim(Shared& S, uint32_t want, Batch& b) {
   std::lock_guard<std::mutex> lk(S.mu);
@@ -256,7 +258,8 @@ void device_thread(Shared& S, khb_ctx* ctx) {
                                                : (int)std::max(2u, std::min(16u, std::thread::hardware_concurrency()));
   int depth = std::max(1, std::min(S.cfg.queue_depth, 2));
   if (depth > 1) {
-    // the second slot's scratch (~35 GB) up front; without it the device runs one batch at a time
+    // the second slot's scratch (~26 GB at the default lanes) up front; without it the device runs one
+    // batch at a time
     const int rrc = khb_reserve_slots(ctx, depth);
     if (rrc == KHB_ENOMEM) {
       depth = 1;
@@ -271,7 +274,7 @@ void device_thread(Shared& S, khb_ctx* ctx) {
   const uint32_t cap = std::min<uint32_t>(khb_candidate_capacity(ctx), (uint32_t)cbuf.size());
   std::vector<Batch> ring(depth + 1);
   std::deque<Batch> parts;    // rescan parts of overflowed batches, submitted before new chunks
-  std::vector<std::pair<double, double>> busy;
+  BusyUnion busy;
   int next = 0;               // ring slots are used and released in FIFO order
   auto take = [&]() { const int i = next; next = (next + 1) % (int)ring.size(); return i; };
   auto stopped = [&]() { std::lock_guard<std::mutex> lk(S.mu); return S.stop; };
@@ -320,7 +323,7 @@ void device_thread(Shared& S, khb_ctx* ctx) {
     pre = -1;
     if (rc) continue;
     const Batch& b = ring[i];
-    busy.emplace_back(st.launch_begin_ms, st.launch_end_ms);
+    busy.add(st.launch_begin_ms, st.launch_end_ms);
     const bool overflow = st.n_cand > cap;
     if (overflow) {
       Batch lo, hi;
@@ -365,7 +368,7 @@ void device_thread(Shared& S, khb_ctx* ctx) {
     if (q.empty()) fill();     // rescan parts left after the last batch
   }
   std::lock_guard<std::mutex> lk(S.mu);
-  S.stats.busy_seconds += union_ms(busy) * 1e-3;
+  S.stats.busy_seconds += busy.ms() * 1e-3;
 }
 
 }  // namespace
