@@ -59,9 +59,10 @@ enum : int {
 };
 constexpr bool is_gated(int m) { return m == kScanG || m == kScanG1; }
 #ifndef KHB_F9WALK
-// 1: the gated scan in 9 x 29-bit limbs (walk_group_g9).  Measured on MI355X: 596 instead of 706
-// VALU instructions per giant step, but VALUBusy 80 % instead of 91 % and 46.8-47.3 vs 47.2-47.6
-// G steps/s (profiles/r02_f9_walk.md), so the product keeps the 8 x 32 walk_group_g.
+// 1: the gated scan in 9 x 29-bit limbs (walk_group_g9, scan_f9.hpp; `make variants` only).  Fewer
+// VALU instructions than the 8 x 32 walk but slower on MI355X in every form tried: 2-4.6 % at 3 and 4
+// waves/SIMD, with a lower shader clock (profiles/r02_f9_walk.md, r03c_f9_ab.txt,
+// r03_calibration/f9_w3_ab.txt), so the product keeps the 8 x 32 walk_group_g.
 #define KHB_F9WALK 0
 #endif
 constexpr bool is_f9(int m) { return (KHB_F9WALK && is_gated(m)) || m == kDumpG; }   // walk in 9 x 29 limbs (fe29.hpp)
