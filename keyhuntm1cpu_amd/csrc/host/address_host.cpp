@@ -406,9 +406,21 @@ void device_loop(AddrShared& S, int device) {
   auto submit = [&](ABatch& b) {
     return khb_addr_submit(ctx, b.centres.data(), (uint32_t)b.bases.size(), 0, groups, S.cfg.search);
   };
+  // both submission slots up front; on KHB_ENOMEM (large targets or many devices' worth of scratch)
+  // one launch at a time instead of failing (advisor r2)
+  size_t depth = 2;
+  if ((rc = khb_reserve_slots(ctx, 2)) == KHB_ENOMEM) {
+    depth = 1;
+    rc = 0;
+    std::lock_guard<std::mutex> lk(S.mu);
+    if (S.cb.on_warning) S.cb.on_warning("[W] no device memory for a second submission slot: one batch in flight");
+  } else if (rc) {
+    khb_close(ctx);
+    return fail(rc, "khb_reserve_slots");
+  }
   std::vector<khb_addr_hit> hits(1u << 18);
   std::deque<int> q;
-  while (q.size() < 2) {
+  while (q.size() < depth) {
     const int i = take();
     if (!prepare(ring[i])) break;
     if ((rc = submit(ring[i]))) { fail(rc, "khb_addr_submit"); break; }

@@ -77,6 +77,7 @@ struct AddrCallbacks {
   std::function<void(const AddrFound&)> on_found;             // called in range order per batch
   std::function<void(const U256& base, int device)> on_chunk;  // "Base key: ..." progress
   std::function<bool()> stop;                                  // polled between batches
+  std::function<void(const std::string&)> on_warning;          // e.g. the depth-1 fallback
 };
 
 // Sequential (or -R random) search over the range; returns 0 or a KHB_E* / -100 code with *err.

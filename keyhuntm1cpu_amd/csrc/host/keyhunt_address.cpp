@@ -112,6 +112,10 @@ int run_address_mode(const AddressCli& o) {
   std::atomic<uint64_t> keys_done{0};
   AddrCallbacks cb;
   cb.on_found = [&](const AddrFound& f) { writekey(f, out_mu); };
+  cb.on_warning = [&](const std::string& m) {
+    std::lock_guard<std::mutex> lk(out_mu);
+    fprintf(stderr, "%s\n", m.c_str());
+  };
   cb.on_chunk = [&](const U256& base, int device) {
     if (o.quiet) return;
     std::lock_guard<std::mutex> lk(out_mu);

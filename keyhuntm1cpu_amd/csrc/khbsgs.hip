@@ -150,6 +150,9 @@ namespace {
 
 int hip_fail(khb_ctx* c, hipError_t e) {
   if (c) c->last_hip = (int)e;
+  // The runtime keeps the last error for hipGetLastError: a failed allocation the caller recovers
+  // from (khb_reserve_slots -> depth 1) would otherwise fail the next launch check of khb_submit.
+  (void)hipGetLastError();
   return e == hipErrorOutOfMemory ? KHB_ENOMEM : KHB_EHIP;
 }
 #define KHB_TRY(c, x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return hip_fail((c), e_); } while (0)
@@ -228,6 +231,10 @@ int ensure_centres(khb_ctx* c, Slot& S, uint32_t n) {
 // The slot the next submission uses (KHB_EBUSY when every slot is in flight).
 Slot* next_slot(khb_ctx* c, int& rc) {
   if (c->queued >= kQueueDepth) { rc = KHB_EBUSY; return nullptr; }
+  // With nothing in flight the ring restarts at slot 0 (allocated by khb_open), so a caller that keeps
+  // one submission in flight -- the depth-1 fallback after KHB_ENOMEM from khb_reserve_slots -- never
+  // touches slot 1.  Collect order stays submission order.
+  if (c->queued == 0) c->head = 0;
   Slot& S = c->slot[(c->head + c->queued) % kQueueDepth];
   rc = ensure_slot(c, S);
   return rc ? nullptr : &S;

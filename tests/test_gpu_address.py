@@ -220,3 +220,15 @@ def test_addr_search_ragged_queue():
     assert sorted(k for k, _, _ in found) == sorted(picks)
     assert st["chunks"] == 75 and st["keys"] == 75 * n_seq
     assert st["launches"] == 3
+
+
+def test_addr_search_falls_back_to_depth_one(keys):
+    """the address loop reserves both submission slots; when the second does not fit (lanes
+    sized so one slot's scratch takes 60 % of HBM) it warns and runs one launch at a time, and still
+    finds puzzles 1..24 over two batches (4,098 chunks of 2^12 keys, 4,096 per batch)."""
+    from tests.test_gpu_depth import _one_slot_lanes
+    A = khhost.Addr(_text("1to32.txt"), n_seq=1 << 12, gpl=4)
+    found, st = A.search(1, (1 << 24) + (1 << 13), search=2, lanes=_one_slot_lanes())
+    got = sorted(k for k, c, _ in found)
+    assert got == sorted(int(keys[str(n)]["key"], 16) for n in range(1, 25))
+    assert st["chunks"] == 4098 and st["launches"] == 2

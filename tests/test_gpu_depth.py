@@ -151,3 +151,58 @@ def test_scan_refused_while_submission_pending():
         assert 0 <= st0.launch_begin_ms < st0.launch_end_ms <= st1.launch_begin_ms < st1.launch_end_ms
         assert abs((st0.launch_end_ms - st0.launch_begin_ms) - st0.kernel_ms) < 0.05
     t.close()
+
+
+def _one_slot_lanes() -> int:
+    """Lanes whose scratch (kBatch x 515 entries of 32 B per lane) takes 60 % of the device's HBM: one
+    submission slot fits, a second cannot."""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")                      # already loaded by libkhbsgs
+    free, total = C.c_size_t(), C.c_size_t()
+    assert hip.hipSetDevice(0) == 0 and hip.hipMemGetInfo(C.byref(free), C.byref(total)) == 0
+    total = total.value
+    per_lane = 32 * khbsgs.groups_per_item() * 515
+    return int(0.6 * total / per_lane) // 256 * 256
+
+
+def test_second_slot_enomem_leaves_one_slot_usable():
+    """khb_reserve_slots on a context whose second slot does not fit returns KHB_ENOMEM and
+    frees the partial slot; the context still scans with one submission in flight (the key's chunk
+    gives its true hit)."""
+    from keyhuntm1cpu_amd.khbsgs import Engine, KhbError
+    t = khhost.Tables("0x100000000", 1, threads=8)
+    tgt = khhost.pubkey(0x2000000000123457)
+    try:
+        with Engine(0, lanes=_one_slot_lanes()) as e:
+            bf, nb, bits, h = t.bloom_concat(1)
+            e.load_bloom(bf, nb, bits, h)
+            e.load_giant_table(t.giant_table())
+            offs, gpl = t.lane_offsets()
+            e.load_lane_offsets(offs, gpl)
+            with pytest.raises(KhbError, match="out of memory"):
+                e.reserve_slots(2)
+            e.reserve_slots(1)                      # slot 0 is intact
+            cands, _, st = e.scan(t.chunk_centre(0x2000000000000000, tgt), 0, t.cycles)
+            assert [a for _, a in cands] and st.giant_steps == t.cycles * 1024
+    finally:
+        t.close()
+
+
+def test_engine_falls_back_to_depth_one():
+    """the search engine asks for two slots; when the second does not fit it warns and runs
+    one batch at a time instead of failing, and still finds every key."""
+    import json
+    import os
+    gold = os.path.join(os.path.dirname(__file__), "golden", "puzzle_keys.json")
+    with open(gold) as f:
+        keys = json.load(f)
+    ns = [26, 27, 28]
+    t = khhost.Tables(hex(1 << 24), 1, threads=8)
+    try:
+        targets = [khhost.parse_pubkey(keys[str(n)]["pubkey"])[0] for n in ns]
+        with khhost.Session(t, lanes=_one_slot_lanes(), chunks_per_batch=2) as s:
+            res, st = s.run(targets, 1 << (ns[0] - 1), 1 << ns[-1])
+        assert res == [int(keys[str(n)]["key"], 16) for n in ns]
+        assert st["launches"] >= 3                   # [2^25, 2^28) is 7 chunks of 2N = 2^25: 4 batches
+    finally:
+        t.close()
