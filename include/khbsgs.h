@@ -96,6 +96,10 @@ int khb_reserve_slots(khb_ctx* ctx, int depth);
  * of the caller's overflow path (stats.n_cand > capacity -> rescan in parts). */
 int khb_set_candidate_capacity(khb_ctx* ctx, uint32_t cap);
 uint32_t khb_candidate_capacity(const khb_ctx* ctx);
+/* Bloom-hit ring entries a -m address launch keeps: min(khb_candidate_capacity, 2^18).  As for the
+ * candidates, stats.n_cand > capacity means "rescan the submission in parts" (every hit must reach
+ * the host's searchbinary, keyhunt.cpp:2716-2937). */
+uint32_t khb_addr_hit_capacity(const khb_ctx* ctx);
 /* Restart the context's clock (khb_stats.launch_begin_ms / launch_end_ms); KHB_EBUSY while a
  * submission is in flight. */
 int khb_reset_epoch(khb_ctx* ctx);

@@ -107,12 +107,15 @@ void khh_addr_giant_table(const khh_addr* a, uint8_t out[513 * 64]);
 uint32_t khh_addr_lane_offsets(const khh_addr* a, uint8_t* out /* n*64, may be NULL */, uint32_t* gpl);
 /* Sequential (random_chunks = 0) or -R search of [start, end) with search 0/1/2 (-l).  Found keys
  * (32 B BE each) with compressed flags and rmd160s, in discovery order; *n_found may exceed cap.
- * stats_out (nullable, 7): [0]=chunks [1]=keys [2]=bloom hits [3]=degenerate groups [4]=kernel us
- * [5]=launches [6]=average shader clock of the launches in kHz. */
+ * stats_out (nullable, 8): [0]=chunks [1]=keys [2]=bloom hits [3]=degenerate groups [4]=kernel us
+ * [5]=launches [6]=average shader clock of the launches in kHz [7]=rescans (launches whose bloom hits
+ * overflowed khb_addr_hit_capacity and were rescanned in parts). */
 int khh_addr_search(const khh_addr* a, const uint8_t start_be[32], const uint8_t end_be[32], int search,
                     int random_chunks, const int* devices, int n_devices, uint32_t lanes, uint64_t max_chunks,
                     uint8_t* keys_be, uint8_t* compressed, uint8_t* rmd, uint32_t cap, uint32_t* n_found,
                     uint64_t* stats_out, char* err, size_t errlen);
+/* Tests: bloom-hit ring capacity of the search's launches (0 = the library default, 2^18). */
+int khh_addr_set_hit_capacity(khh_addr* a, uint32_t cap);
 /* hash160 of a public key (x||y BE) and its P2PKH address (out_addr >= 36 bytes) */
 void khh_hash160(const uint8_t xy[64], int compressed, uint8_t out[20]);
 void khh_rmd_to_address(const uint8_t rmd[20], char* out_addr);

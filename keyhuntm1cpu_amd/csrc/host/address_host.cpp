@@ -352,7 +352,8 @@ void device_loop(AddrShared& S, int device) {
   const uint32_t groups = (uint32_t)(S.cfg.n_seq / 1024);
   const std::vector<uint8_t> gtab = S.G.table_be(), offs = S.G.offs_be();
   const BloomGeom bg = S.T.bloom.geom();
-  if ((rc = khb_load_giant_table(ctx, gtab.data())) ||
+  if ((S.cfg.hit_cap && (rc = khb_set_candidate_capacity(ctx, S.cfg.hit_cap))) ||
+      (rc = khb_load_giant_table(ctx, gtab.data())) ||
       (rc = khb_load_lane_offsets(ctx, offs.data(), (uint32_t)S.G.offs.size(), S.G.gpl)) ||
       (rc = khb_load_addr_bloom(ctx, S.T.bloom.bf.data(), bg.bytes_per_sub, bg.bits, bg.hashes))) {
     khb_close(ctx);
@@ -369,14 +370,48 @@ void device_loop(AddrShared& S, int device) {
   struct ABatch {
     std::vector<U256> bases;
     std::vector<uint8_t> centres;
+    uint32_t group_begin = 0, group_count = 0;   // group range of every chunk (0 = the whole chunk)
+    bool part = false;                           // a rescan part of a batch whose hits overflowed
   };
   ABatch ring[3];
   int next = 0;
   auto take = [&]() { const int i = next; next = (next + 1) % 3; return i; };
   const U256 half = S.G.stride * 512u;
+  // A batch whose bloom hits overflowed the ring is rescanned in two parts (by chunks, or one chunk by
+  // a gpl-aligned group range), queued ahead of new chunks: every hit reaches confirm_hit, as every
+  // hit reaches searchbinary in the reference (keyhunt.cpp:2716-2937).
+  std::deque<ABatch> parts;
+  auto split = [&](const ABatch& b, ABatch& lo, ABatch& hi) {
+    const size_t n = b.bases.size();
+    const uint32_t g0 = b.group_begin, gc = b.group_count ? b.group_count : groups;
+    auto part = [&](ABatch& o, size_t j0, size_t j1, uint32_t pb, uint32_t pc) {
+      o.bases.assign(b.bases.begin() + j0, b.bases.begin() + j1);
+      o.centres.assign(b.centres.begin() + 64 * j0, b.centres.begin() + 64 * j1);
+      o.group_begin = pb;
+      o.group_count = pc;
+      o.part = true;
+    };
+    if (n > 1) {
+      part(lo, 0, n / 2, g0, gc);
+      part(hi, n / 2, n, g0, gc);
+      return true;
+    }
+    if (n == 0 || gc <= S.G.gpl) return false;
+    const uint32_t h = (gc / 2 + S.G.gpl - 1) / S.G.gpl * S.G.gpl;
+    part(lo, 0, 1, g0, h);
+    part(hi, 0, 1, g0 + h, gc - h);
+    return true;
+  };
   auto prepare = [&](ABatch& b) {
     b.bases.clear();
     if (S.cb.stop && S.cb.stop()) return false;
+    if (!parts.empty()) {
+      b = std::move(parts.front());
+      parts.pop_front();
+      return true;
+    }
+    b.group_begin = b.group_count = 0;
+    b.part = false;
     {
       std::lock_guard<std::mutex> lk(S.mu);
       if (S.rc) return false;
@@ -404,7 +439,8 @@ void device_loop(AddrShared& S, int device) {
     return true;
   };
   auto submit = [&](ABatch& b) {
-    return khb_addr_submit(ctx, b.centres.data(), (uint32_t)b.bases.size(), 0, groups, S.cfg.search);
+    return khb_addr_submit(ctx, b.centres.data(), (uint32_t)b.bases.size(), b.group_begin,
+                           b.group_count ? b.group_count : groups, S.cfg.search);
   };
   // both submission slots up front; on KHB_ENOMEM (large targets or many devices' worth of scratch)
   // one launch at a time instead of failing (advisor r2)
@@ -426,12 +462,10 @@ void device_loop(AddrShared& S, int device) {
     if ((rc = submit(ring[i]))) { fail(rc, "khb_addr_submit"); break; }
     q.push_back(i);
   }
+  const uint32_t acap = std::min<uint32_t>(khb_addr_hit_capacity(ctx), (uint32_t)(1u << 18));
   int pre = -1;
   while (!q.empty()) {
-    if (pre < 0 && !rc) {
-      const int k = take();
-      if (prepare(ring[k])) pre = k;                  // overlaps the GPU scan
-    }
+    if (pre < 0 && !rc && prepare(ring[next])) pre = take();   // overlaps the GPU scan
     const int i = q.front();
     q.pop_front();
     khb_stats st{};
@@ -446,7 +480,30 @@ void device_loop(AddrShared& S, int device) {
     pre = -1;
     if (rc) continue;
     const ABatch& b = ring[i];
-    const uint32_t nh = st.n_cand < hits.size() ? st.n_cand : (uint32_t)hits.size();
+    if (st.n_cand > acap) {              // the ring kept only acap hits: rescan the batch in parts
+      ABatch lo, hi;
+      if (!split(b, lo, hi)) {
+        fail(-100, "bloom hit ring overflow on a single work item (target bloom too full)");
+        rc = -100;
+        continue;
+      }
+      parts.push_front(std::move(hi));
+      parts.push_front(std::move(lo));
+      {
+        std::lock_guard<std::mutex> lk(S.mu);
+        S.stats.launches++;
+        S.stats.rescans++;
+        S.stats.kernel_seconds += st.kernel_ms * 1e-3;
+        if (!b.part) S.stats.chunks += b.bases.size();
+      }
+      if (q.empty() && pre < 0 && prepare(ring[next])) {    // keep the device busy with the parts
+        const int k = take();
+        if ((rc = submit(ring[k]))) fail(rc, "khb_addr_submit");
+        else q.push_back(k);
+      }
+      continue;
+    }
+    const uint32_t nh = st.n_cand;
     std::sort(hits.begin(), hits.begin() + nh, [](const khb_addr_hit& x, const khb_addr_hit& y) {
       if (x.job != y.job) return x.job < y.job;
       if (x.group != y.group) return x.group < y.group;
@@ -462,7 +519,7 @@ void device_loop(AddrShared& S, int device) {
     }
     std::lock_guard<std::mutex> lk(S.mu);
     S.stats.launches++;
-    S.stats.chunks += b.bases.size();
+    if (!b.part) S.stats.chunks += b.bases.size();
     S.stats.keys += st.giant_steps;
     S.stats.hits += st.n_cand;
     S.stats.degenerate += st.n_degenerate;
@@ -474,10 +531,6 @@ void device_loop(AddrShared& S, int device) {
     S.stats.found += found.size();
     if (S.cb.on_found)
       for (const AddrFound& f : found) S.cb.on_found(f);
-    if (st.n_cand > hits.size() && !S.rc) {
-      S.rc = -100;
-      S.err = "bloom hit buffer overflow (target bloom too full for this batch)";
-    }
   }
   khb_close(ctx);
 }

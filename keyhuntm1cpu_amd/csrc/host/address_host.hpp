@@ -58,6 +58,7 @@ struct AddrConfig {
   uint32_t lanes = 0;                  // 0 = library default
   uint32_t gpl = 16;                   // groups per GPU lane
   uint64_t max_chunks = 0;             // 0 = until the range is exhausted
+  uint32_t hit_cap = 0;                // tests: the launch's bloom-hit capacity (0 = library default)
 };
 
 struct AddrFound {
@@ -68,6 +69,7 @@ struct AddrFound {
 
 struct AddrStats {
   uint64_t launches = 0, chunks = 0, keys = 0, hits = 0, found = 0, degenerate = 0;
+  uint64_t rescans = 0;            // launches whose bloom hits overflowed the ring (rescanned in parts)
   double kernel_seconds = 0;
   double shader_mhz_sum = 0;       // sum of the launches' average shader clocks (khb_stats.shader_mhz)
   uint64_t shader_mhz_n = 0;

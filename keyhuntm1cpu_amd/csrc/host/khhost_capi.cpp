@@ -21,6 +21,7 @@ struct khh_addr {
   AddrTargets T;
   AddrGen G;
   uint64_t n_seq = 0;
+  uint32_t hit_cap = 0;      // tests: bloom-hit ring capacity per launch (0 = library default)
 };
 
 static void set_err(char* err, size_t n, const std::string& m) {
@@ -348,6 +349,7 @@ int khh_addr_search(const khh_addr* a, const uint8_t start_be[32], const uint8_t
   cfg.lanes = lanes;
   cfg.gpl = a->G.gpl;
   cfg.max_chunks = max_chunks;
+  cfg.hit_cap = a->hit_cap;
   cfg.devices.clear();
   for (int i = 0; i < n_devices; ++i) cfg.devices.push_back(devices[i]);
   if (cfg.devices.empty()) cfg.devices.push_back(0);
@@ -373,9 +375,16 @@ int khh_addr_search(const khh_addr* a, const uint8_t start_be[32], const uint8_t
     stats_out[4] = (uint64_t)(st.kernel_seconds * 1e6);
     stats_out[5] = st.launches;
     stats_out[6] = st.shader_mhz_n ? (uint64_t)(1e3 * st.shader_mhz_sum / st.shader_mhz_n) : 0;
+    stats_out[7] = st.rescans;
   }
   if (rc) set_err(err, errlen, e);
   return rc;
+}
+
+int khh_addr_set_hit_capacity(khh_addr* a, uint32_t cap) {
+  if (!a) return KHB_EINVAL;
+  a->hit_cap = cap;
+  return KHB_OK;
 }
 
 void khh_hash160(const uint8_t xy[64], int compressed, uint8_t out[20]) {

@@ -362,6 +362,10 @@ int khb_set_candidate_capacity(khb_ctx* c, uint32_t cap) {
 
 uint32_t khb_candidate_capacity(const khb_ctx* c) { return c ? c->cand_cap : 0; }
 
+uint32_t khb_addr_hit_capacity(const khb_ctx* c) {
+  return c ? (c->cand_cap < kAddrHitCap ? c->cand_cap : kAddrHitCap) : 0;
+}
+
 int khb_reset_epoch(khb_ctx* c) {
   if (!c) return KHB_EINVAL;
   if (c->queued) return KHB_EBUSY;
@@ -707,7 +711,7 @@ int khb_addr_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_
   A.bloom = c->d_abloom;
   A.geom = c->ageom;
   A.ahits = S.d_ahits;
-  A.ahit_cap = kAddrHitCap;
+  A.ahit_cap = khb_addr_hit_capacity(c);
   const uint32_t blocks = c->lanes / kBlock;
   KHB_TRY(c, hipEventRecord(S.ev0, S.stream));
   launch_addr(search == 0 ? kAddrU : search == 1 ? kAddrC : kAddrB, blocks, S.stream, A);
@@ -730,7 +734,8 @@ int khb_addr_collect(khb_ctx* c, khb_addr_hit* hits, uint32_t cap, khb_stats* st
   c->queued--;
   KHB_TRY(c, hipStreamSynchronize(S.stream));
   const uint32_t nh = S.h_counters[0], nd = S.h_counters[1];
-  uint32_t take = nh < kAddrHitCap ? nh : kAddrHitCap;
+  const uint32_t acap = khb_addr_hit_capacity(c);
+  uint32_t take = nh < acap ? nh : acap;
   if (take > cap) take = cap;
   if (take && hits) KHB_TRY(c, hipMemcpy(hits, S.d_ahits, sizeof(khb_addr_hit) * take, hipMemcpyDeviceToHost));
   const uint64_t steps = walked_groups(S) * KHB_GROUP;

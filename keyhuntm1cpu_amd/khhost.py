@@ -77,6 +77,7 @@ def lib() -> C.CDLL:
         L.khh_addr_search.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int, C.c_int, P(C.c_int), C.c_int,
                                       C.c_uint32, C.c_uint64, C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint32,
                                       P(C.c_uint32), P(C.c_uint64), C.c_char_p, C.c_size_t]
+        L.khh_addr_set_hit_capacity.argtypes = [C.c_void_p, C.c_uint32]
         L.khh_hash160.argtypes = [C.c_char_p, C.c_int, C.c_char_p]
         L.khh_rmd_to_address.argtypes = [C.c_char_p, C.c_char_p]
         _lib = L
@@ -351,6 +352,11 @@ class Addr:
         lib().khh_addr_lane_offsets(self.h, out, C.byref(g))
         return out.raw, int(g.value)
 
+    def set_hit_capacity(self, cap: int) -> None:
+        """Tests: the launches' bloom-hit ring capacity (0 = default 2^18); overflow -> rescan in parts."""
+        if lib().khh_addr_set_hit_capacity(self.h, cap):
+            raise KhhError("khh_addr_set_hit_capacity")
+
     def search(self, start: int, end: int, search: int = 2, devices=(0,), lanes: int = 0, max_chunks: int = 0,
                random_chunks: bool = False, cap: int = 4096):
         """Found [(key, compressed, rmd160)] in discovery order, plus stats."""
@@ -358,7 +364,7 @@ class Addr:
         comp = C.create_string_buffer(cap)
         rmd = C.create_string_buffer(20 * cap)
         nf = C.c_uint32(0)
-        st = (C.c_uint64 * 7)()
+        st = (C.c_uint64 * 8)()
         devs = (C.c_int * len(devices))(*devices)
         err = C.create_string_buffer(256)
         rc = lib().khh_addr_search(self.h, _b32(start), _b32(end), search, 1 if random_chunks else 0, devs,
@@ -369,4 +375,4 @@ class Addr:
         found = [(int.from_bytes(keys.raw[32 * i:32 * i + 32], "big"), bool(comp.raw[i]), rmd.raw[20 * i:20 * i + 20])
                  for i in range(n)]
         return found, {"chunks": st[0], "keys": st[1], "hits": st[2], "degenerate": st[3], "kernel_s": st[4] / 1e6,
-                       "launches": st[5], "shader_mhz": st[6] / 1e3}
+                       "launches": st[5], "shader_mhz": st[6] / 1e3, "rescans": st[7]}

@@ -232,3 +232,18 @@ def test_addr_search_falls_back_to_depth_one(keys):
     got = sorted(k for k, c, _ in found)
     assert got == sorted(int(keys[str(n)]["key"], 16) for n in range(1, 25))
     assert st["chunks"] == 4098 and st["launches"] == 2
+
+
+def test_addr_hit_overflow_rescans_and_finds_every_key(keys):
+    """Every bloom hit must reach the host check (keyhunt.cpp:2716-2937 -> searchbinary).  With a
+    16-entry hit ring the 16-chunk batch overflows (24 true hits), and so does chunk 0 on its own
+    (puzzles 1..20); the address loop rescans in parts -- by chunks, then chunk 0's group ranges (its
+    first 16-group work item holds puzzles 1..14) -- instead of failing, and still finds puzzles 1..24,
+    each once, with the chunk and key counts of one pass."""
+    A = khhost.Addr(_text("1to32.txt"), n_seq=1 << 20)
+    A.set_hit_capacity(16)
+    found, st = A.search(1, 1 << 24, search=2, lanes=65536)
+    got = sorted(k for k, c, _ in found)
+    assert got == sorted(int(keys[str(n)]["key"], 16) for n in range(1, 25))
+    assert st["rescans"] > 0
+    assert st["chunks"] == 16 and st["keys"] == 1 << 24
