@@ -257,15 +257,19 @@ def main():
         print(f"[bench] ERROR: device-busy {bmax:.3f} ms per step exceeds the wall time {wall_ms:.3f} ms",
               file=sys.stderr, flush=True)
         raise SystemExit(3)
+    time_basis = ("kernel_busy_ms_per_step: union of the k_giant_scan launch intervals over the timed "
+                  "steps (HIP events on each launch's stream) / steps; <= ms_per_step")
+    if bmax <= 0:    # no launch interval was timed (events unavailable): fall back to the wall time
+        bmax = wall_ms
+        time_basis = "ms_per_step (the launches' event intervals were unavailable)"
     achieved = OPS_PER_STEP * per_launch_steps / (bmax * 1e-3) / 1e12
-    achieved_launch = OPS_PER_STEP * per_launch_steps / (kmax * 1e-3) / 1e12
+    achieved_launch = OPS_PER_STEP * per_launch_steps / (max(kmax, 1e-9) * 1e-3) / 1e12
     executed = EXEC_OPS_PER_STEP * per_launch_steps / (bmax * 1e-3) / 1e12
     roofline = {"bound": "valu", "unit": "Tops/s", "achieved": round(achieved, 3), "peak": PEAK_MULOPS_T,
                 "frac": round(achieved / PEAK_MULOPS_T, 4), "traffic": None,
                 "ops": "32-bit multiply-class lane ops of the reference algorithm (v_mad_u64_u32 / v_mul_lo_u32)",
                 "ops_per_giant_step": round(OPS_PER_STEP, 2), "kernel": "k_giant_scan",
-                "time_basis": "kernel_busy_ms_per_step: union of the k_giant_scan launch intervals over the timed "
-                              "steps (HIP events on each launch's stream) / steps; <= ms_per_step",
+                "time_basis": time_basis,
                 "kernel_busy_ms_per_step": round(bmax, 3),
                 "shader_mhz_avg": round(st["shader_mhz"], 1),
                 "kernel_ms_avg": round(kmax, 3),
