@@ -247,3 +247,14 @@ def test_addr_hit_overflow_rescans_and_finds_every_key(keys):
     assert got == sorted(int(keys[str(n)]["key"], 16) for n in range(1, 25))
     assert st["rescans"] > 0
     assert st["chunks"] == 16 and st["keys"] == 1 << 24
+
+
+def test_addr_search_two_contexts_share_the_cursor(keys):
+    """-m address with two device threads (-g 0,0: two contexts on one GPU) pulling chunks from one
+    shared cursor (address_host.cpp device_loop, keyhunt.cpp:2586-2937 threads): puzzles 1..24 are each
+    found exactly once and the 16 chunks of [1, 2^24) are each scanned once."""
+    A = khhost.Addr(_text("1to32.txt"), n_seq=1 << 20)
+    found, st = A.search(1, 1 << 24, search=2, devices=(0, 0), lanes=16384)
+    got = sorted(k for k, c, _ in found)
+    assert got == sorted(int(keys[str(n)]["key"], 16) for n in range(1, 25))
+    assert st["chunks"] == 16 and st["keys"] == 1 << 24
