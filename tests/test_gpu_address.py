@@ -258,3 +258,15 @@ def test_addr_search_two_contexts_share_the_cursor(keys):
     got = sorted(k for k, c, _ in found)
     assert got == sorted(int(keys[str(n)]["key"], 16) for n in range(1, 25))
     assert st["chunks"] == 16 and st["keys"] == 1 << 24
+
+
+def test_addr_random_chunk_mode_finds_the_key(keys):
+    """-m address -R: chunks of n keys start at random keys of [start, end) (keyhunt.cpp:2586-2937 with
+    FLAGRANDOM); a range two chunks wide around puzzle 24's key is covered by each chunk with
+    probability ~1/2, so 40 random chunks find it."""
+    A = khhost.Addr(_text("1to32.txt"), n_seq=1 << 16)
+    key = int(keys["24"]["key"], 16)
+    found, st = A.search(key - (1 << 16) + 1, key + (1 << 16), search=2, lanes=16384, max_chunks=40,
+                         random_chunks=True)
+    assert key in [k for k, c, _ in found]
+    assert 1 <= st["chunks"] <= 40

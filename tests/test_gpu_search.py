@@ -276,3 +276,21 @@ def test_cli_save_read_table_files(tmp_path):
     assert "[+] Reading bP Table from file keyhunt_bsgs_2_1.tbl" in r2.stdout
     assert "Writing" not in r2.stdout
     assert "privkey 3d94cd64" in r2.stdout
+
+
+def test_random_chunk_mode_finds_the_key(keys):
+    """-R (keyhunt.cpp:3824-3844 with FLAGRANDOM): every claimed chunk starts at a random key of
+    [start, end) (getrandom, Random.cpp:133-145) and is scanned whole.  The range is two chunks wide
+    around puzzle 30's key, so each random chunk covers it with probability ~1/2; 40 chunks find it
+    (miss probability ~2^-40) and the search stops at the find."""
+    t = khhost.Tables("0x100000", 1, threads=8)      # one chunk = 2N = 2^21 keys
+    try:
+        key = int(keys["30"]["key"], 16)
+        xy = khhost.parse_pubkey(keys["30"]["pubkey"])[0]
+        two_n = 1 << 21
+        with khhost.Session(t, chunks_per_batch=4) as s:
+            res, st = s.run([xy], key - two_n + 1, key + two_n, max_chunks=40, random_chunks=True)
+        assert res == [key]
+        assert 1 <= st["chunks"] <= 40
+    finally:
+        t.close()
