@@ -9,8 +9,9 @@
 #   pair_patch.py: the paired reduction (exact; slower at 4 waves because it spills).
 #   defer_patch.py: the gate tested one walk step after its loads, pending x pair in registers.
 #   nonop_patch.py: the carry-hazard s_nop pads removed (timing only).
+#   block_patch.py: KHB_BLOCK threads per workgroup.
 #   scr_patch.py: KHB_SCR_MASK=m keeps the prefix scratch in (i & m) entries per group (no HBM stream).
-# Usage: tools/experiments/calib_build.sh pad|rm|scr|pair|defer|nonop <name> [-DKEY=VAL ...]
+# Usage: tools/experiments/calib_build.sh pad|rm|scr|pair|defer|nonop|block <name> [-DKEY=VAL ...]
 set -e
 KIND=$1; NAME=$2; shift 2
 S1=keyhuntm1cpu_amd/csrc/device/fe_asm.hpp
