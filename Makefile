@@ -14,7 +14,7 @@ BINDIR   := $(PKG)/bin
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wno-unused-result -Wno-unused-value
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -march=x86-64-v3 -Wall -Wextra -Wno-unused-function -Wno-unused-parameter -Wno-unknown-pragmas -pthread
 
-DEV_HDRS  := $(wildcard $(CSRC)/device/*.hpp) $(CSRC)/scan_kernels.hpp $(CSRC)/scan_f9.hpp include/khbsgs.h
+DEV_HDRS  := $(wildcard $(CSRC)/device/*.hpp) $(CSRC)/scan_kernels.hpp include/khbsgs.h
 # libkhbsgs: the C ABI (khbsgs.hip) + one translation unit per group of k_giant_scan instances, so
 # `make -j` compiles the heavy kernels in parallel
 HIP_SRCS  := $(CSRC)/khbsgs.hip $(CSRC)/k_bsgs.hip $(CSRC)/k_addr.hip $(CSRC)/k_baby.hip
@@ -35,13 +35,6 @@ build/hip/%.o: $(CSRC)/%.hip $(DEV_HDRS) | build/hip
 
 $(LIBDIR)/libkhbsgs.so: $(HIP_OBJS) | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_OBJS)
-
-# The same library with the gated scan in 9 x 29-bit limbs (KHB_F9WALK=1, device/fe29.hpp): an
-# alternative build kept parity-tested (tests/test_gpu_f9walk.py); the product uses the 8 x 32 walk.
-build/hip/%_f9.o: $(CSRC)/%.hip $(DEV_HDRS) | build/hip
-	$(HIPCC) $(HIPFLAGS) -DKHB_F9WALK=1 -c -o $@ $<
-$(LIBDIR)/libkhbsgs_f9.so: build/hip/khbsgs_f9.o build/hip/k_bsgs_f9.o build/hip/k_addr.o build/hip/k_baby.o | $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 build/host/%.o: $(CSRC)/host/%.cpp $(HOST_HDRS) | build/host
 	$(CXX) $(CXXFLAGS) -c -o $@ $<
@@ -64,7 +57,5 @@ clean:
 
 .PHONY: all oracle clean
 
-# Variants, not the product: the 9 x 29-bit walk library (tests/test_gpu_f9walk.py runs when it exists),
-# and ad-hoc A/B builds with tools/build_variant.sh <name> -DKEY=VAL (lib/variants/, tools/perf_variants.py).
-variants: $(LIBDIR)/libkhbsgs_f9.so
-.PHONY: variants
+# Timing-only A/B builds are not the product: tools/build_variant.sh <name> -DKEY=VAL writes
+# lib/variants/libkhbsgs_<name>.so for tools/perf_variants.py.  No test loads them.

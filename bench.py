@@ -52,9 +52,19 @@ EXEC_OPS_PER_STEP = ((2556 + 9) * MUL_OPS + (1023 + 1) * SQR_OPS) / 1024.0 + 2 *
 # Peak of the binding unit: v_mad_u64_u32 issue rate measured on MI355X by tools/microbench/intops2.hip
 # at full occupancy, 57.8 lane-ops/clk/CU at the 2.16 GHz the microbenchmark ran at
 # (profiles/r01_intops2.txt); the same rate at the 2.4 GHz peak engine clock is 35.5 T.
-PEAK_MULOPS_T = float(os.environ.get("KHB_PEAK_MULOPS_T", "32.04"))
-PEAK_CLK_GHZ, PEAK_LANES_PER_CLK_CU, CUS = 2.16, 57.8, 256
-PEAK_MULOPS_T_2P4 = round(PEAK_LANES_PER_CLK_CU * CUS * 2.4e9 / 1e12, 2)
+# The headline peak uses the guide's 2.4 GHz peak engine clock (MI355X_MICROARCH.md): 35.51 T; the same
+# rate at the microbenchmark's 2.16 GHz (32.04 T) and at the launches' own measured shader clock are
+# reported beside it.
+PEAK_LANES_PER_CLK_CU, CUS = 57.8, 256
+PEAK_CLK_GHZ, MICROBENCH_CLK_GHZ = 2.4, 2.16
+
+
+def mulops_peak_t(ghz: float) -> float:
+    return round(PEAK_LANES_PER_CLK_CU * CUS * ghz * 1e9 / 1e12, 2)
+
+
+PEAK_MULOPS_T = mulops_peak_t(PEAK_CLK_GHZ)                   # 35.51
+PEAK_MULOPS_T_2P16 = mulops_peak_t(MICROBENCH_CLK_GHZ)        # 32.04
 HBM_PEAK_GBS = 8000.0
 BSGSD_CPU_MKEYS = 16.9     # the reference's own published BSGS rate (BSGSD.md:52-58, 8 threads)
 
@@ -113,6 +123,37 @@ def cpu_baseline(seconds: float, threads: int, target, base: int):
     return steps / el
 
 
+def init_gloo(dist, rank: int, world: int):
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    # gloo's C++ connect messages go to fd 1; keep stdout for the one JSON line (rank 0)
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.barrier()
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+def launch_check(args, world: int, rank: int, local: int):
+    """--launch-check: the rank layout only (no GPU).  Rank 0 prints every rank's (rank, local, pid)."""
+    if args.launch_check_fail == rank:
+        raise SystemExit(3)
+    import torch.distributed as dist
+    view = {"rank": rank, "local_rank": local, "world": world, "pid": os.getpid()}
+    views = [view]
+    if world > 1:
+        init_gloo(dist, rank, world)
+        views = [None] * world
+        dist.all_gather_object(views, view)
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks": views}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -131,13 +172,24 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=60.0,
                     help="CPU-baseline window (BASELINE.md: 60 s steady state after the table build)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # launcher self-test (tests/test_launch.py): every rank joins the gloo world and rank 0 prints the
+    # ranks' view; no GPU is touched.  --launch-check-fail R makes rank R exit with status 3.
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--launch-check-fail", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.workload == "p130" and args.k != 1:
         raise SystemExit("--workload p130 is BASELINE configs[3]: k = 1")
 
+    # --gpus N: one process per GPU.  Under a launcher (WORLD_SIZE set) this process is one rank and
+    # WORLD_SIZE must equal N; run bare with N > 1, the ranks are started here as child processes before
+    # anything touches the GPU (keyhuntm1cpu_amd/launch.py), and this process only forwards rank 0's line.
+    from keyhuntm1cpu_amd import launch
+    launch.main_or_spawn(args.gpus, sys.argv[1:], os.path.abspath(__file__))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        return launch_check(args, world, rank, local)
     import torch                                   # first: share torch's HIP runtime with our libraries
     import torch.distributed as dist
     ndev = torch.cuda.device_count()
@@ -148,40 +200,47 @@ def main():
         local = local % ndev
     torch.cuda.set_device(local)
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # gloo's C++ connect messages go to fd 1; keep stdout for the one JSON line (rank 0)
-        sys.stdout.flush()
-        saved = os.dup(1)
-        os.dup2(2, 1)
-        try:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
-            dist.barrier()
-        finally:
-            os.dup2(saved, 1)
-            os.close(saved)
+        init_gloo(dist, rank, world)
 
     from keyhuntm1cpu_amd import khhost
-    from keyhuntm1cpu_amd.partition import blocks_fit, rank_range
+    from keyhuntm1cpu_amd.partition import blocks_fit, fit_batch, rank_range
     host_threads = min(16, os.cpu_count() or 1)
     if args.workload == "address":
         return bench_address(args, world, rank, dist, torch)
     t0 = time.time()
     tables = khhost.Tables(None, args.k, threads=host_threads, gpl=4)
     t_build = time.time() - t0
-    if not args.chunks:
+    auto_chunks = not args.chunks
+    from keyhuntm1cpu_amd import khbsgs
+    # chunks that give every lane of the device one work item
+    fill = -(-khbsgs.default_lanes(local) * khbsgs.groups_per_item() // tables.cycles)
+    if auto_chunks:
         # eight work items per lane, as the CLI's auto batch (engine.cpp batch_chunks): waves take
         # items dynamically (KHB_DYN), so a deeper queue keeps every SIMD 3 waves deep until the
         # launch's last items (profiles/r01c_dyn_probe.txt)
-        from keyhuntm1cpu_amd import khbsgs
-        fill = -(-khbsgs.default_lanes(local) * khbsgs.groups_per_item() // tables.cycles)
         args.chunks = max(1, (1 << 30) // (tables.cycles * 1024), 8 * fill)
     two_n = 2 * (tables.n_low)                     # 2N keys per chunk
     per_rank = (args.warmup + args.steps) * args.chunks
+    chunks_note = None
     if args.workload == "p66":
         target = puzzle66_target()
         lo, hi = 1 << 65, 1 << 66
         blocks = blocks_fit(lo, hi, two_n, world, per_rank, PUZZLE66_KEY)
         bad = [r for r, (_, _, ok) in enumerate(blocks) if not ok]
+        if bad and auto_chunks:
+            # -b 66 holds 2^20 chunks of 2^45 keys: split N ways, a long run (many --steps) at the auto
+            # batch would leave some rank's block.  Shrink the batch to whole work items per lane so that
+            # every rank's W + K steps stay inside its block (at least one item per lane), else refuse.
+            shrunk = fit_batch(lo, hi, two_n, world, args.warmup + args.steps, args.chunks, fill, PUZZLE66_KEY)
+            if shrunk:
+                chunks_note = ("auto batch %d chunks per step shrunk to %d (%d work items per lane) so that %d "
+                               "steps fit every rank's -b 66 block" % (args.chunks, shrunk, shrunk // fill,
+                                                                      args.warmup + args.steps))
+                print("[bench] " + chunks_note, file=sys.stderr, flush=True)
+                args.chunks = shrunk
+                per_rank = (args.warmup + args.steps) * args.chunks
+                blocks = blocks_fit(lo, hi, two_n, world, per_rank, PUZZLE66_KEY)
+                bad = [r for r, (_, _, ok) in enumerate(blocks) if not ok]
         if bad:
             s0, e0, _ = blocks[bad[0]]
             raise SystemExit("[bench] -b 66 split %d ways: rank %d's block holds %d steps of %d chunks, %d requested "
@@ -247,10 +306,17 @@ def main():
             dist.destroy_process_group()
         raise SystemExit(3)
 
+    ranges = [(start, end)]
+    if world > 1:
+        ranges = [None] * world
+        dist.all_gather_object(ranges, (start, end))
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
         return
+    if not all(lo <= s0 < e0 <= hi for s0, e0 in ranges):
+        print(f"[bench] ERROR: a rank's block leaves [{hex(lo)}, {hex(hi)})", file=sys.stderr, flush=True)
+        raise SystemExit(3)
     gsps = tot_steps / tmax
     wall_ms = 1e3 * tmax / args.steps
     if bmax > wall_ms * 1.0005:
@@ -265,26 +331,31 @@ def main():
     achieved = OPS_PER_STEP * per_launch_steps / (bmax * 1e-3) / 1e12
     achieved_launch = OPS_PER_STEP * per_launch_steps / (max(kmax, 1e-9) * 1e-3) / 1e12
     executed = EXEC_OPS_PER_STEP * per_launch_steps / (bmax * 1e-3) / 1e12
+    mhz = st["shader_mhz"]
+    peak_at_clock = PEAK_LANES_PER_CLK_CU * CUS * mhz * 1e6 / 1e12 if mhz > 0 else None
     roofline = {"bound": "valu", "unit": "Tops/s", "achieved": round(achieved, 3), "peak": PEAK_MULOPS_T,
                 "frac": round(achieved / PEAK_MULOPS_T, 4), "traffic": None,
                 "ops": "32-bit multiply-class lane ops of the reference algorithm (v_mad_u64_u32 / v_mul_lo_u32)",
                 "ops_per_giant_step": round(OPS_PER_STEP, 2), "kernel": "k_giant_scan",
+                "per": "one GPU (the slowest rank's busy time when n_gpus > 1)",
                 "time_basis": time_basis,
                 "kernel_busy_ms_per_step": round(bmax, 3),
-                "shader_mhz_avg": round(st["shader_mhz"], 1),
+                "shader_mhz_avg": round(mhz, 1),
                 "kernel_ms_avg": round(kmax, 3),
                 "achieved_per_launch": round(achieved_launch, 3),
                 "frac_per_launch": round(achieved_launch / PEAK_MULOPS_T, 4),
-                "peak_basis": "v_mad_u64_u32 %.1f lane-ops/clk/CU x %d CUs at %.2f GHz (profiles/r01_intops2.txt); "
-                              "%.2f T at the 2.4 GHz peak clock" % (PEAK_LANES_PER_CLK_CU, CUS, PEAK_CLK_GHZ,
-                                                                    PEAK_MULOPS_T_2P4),
-                "frac_at_2p4ghz": round(achieved / PEAK_MULOPS_T_2P4, 4)}
+                "peak_basis": "v_mad_u64_u32 %.1f lane-ops/clk/CU (profiles/r01_intops2.txt) x %d CUs at the %.1f GHz "
+                              "peak engine clock (MI355X_MICROARCH.md)" % (PEAK_LANES_PER_CLK_CU, CUS, PEAK_CLK_GHZ),
+                "peak_at_2p16ghz": PEAK_MULOPS_T_2P16,
+                "frac_at_2p16ghz": round(achieved / PEAK_MULOPS_T_2P16, 4),
+                "peak_at_shader_clock": round(peak_at_clock, 3) if peak_at_clock else None,
+                "frac_at_shader_clock": round(achieved / peak_at_clock, 4) if peak_at_clock else None}
     executed_info = {"ops_per_giant_step": round(EXEC_OPS_PER_STEP, 2),
                      "note": "multiply-class work the kernel performs: the reference's field work without the "
                              "3 of 4 inversions the 8-group batch saves and without the two XXH64 the level-0 "
                              "gate skips for 99.96 % of x",
                      "achieved": round(executed, 3), "frac": round(executed / PEAK_MULOPS_T, 4),
-                     "frac_at_2p4ghz": round(executed / PEAK_MULOPS_T_2P4, 4)}
+                     "frac_at_2p16ghz": round(executed / PEAK_MULOPS_T_2P16, 4)}
     pmc_path = os.path.join(REPO, "profiles", "pmc_latest.json")
     if os.path.exists(pmc_path):
         try:
@@ -341,6 +412,12 @@ def main():
                    "chunks_per_step": args.chunks, "giant_steps_per_step": per_launch_steps,
                    "parallelism": "range-partition x%d" % world, "table_build_s": round(t_build, 2),
                    "rank0_range": [hex(start), hex(end)],
+                   "rank_ranges": [[hex(a), hex(b)] for a, b in ranges],
+                   "timed_ranges": [[hex(a + args.warmup * args.chunks * two_n),
+                                     hex(a + (args.warmup + args.steps) * args.chunks * two_n)] for a, _ in ranges],
+                   "launcher": ("bench.py child ranks" if os.environ.get("KHB_BENCH_CHILD") else
+                                "external (WORLD_SIZE set)") if world > 1 else "none",
+                   "batch_note": chunks_note,
                    "ref_keys_per_s": "%.3e" % (gsps * 2 * tables.m),
                    "candidates": st["candidates"], "found": [hex(r) if r else None for r in res]},
         "roofline": roofline,

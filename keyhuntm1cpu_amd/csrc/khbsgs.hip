@@ -131,7 +131,6 @@ struct khb_ctx {
   uint32_t gate1_log2 = KHB_GATE1;     // khb_set_gate_stage1: fold size for gates loaded later
   uint32_t gate_mask = 0, gate_probes = 0;
   AffPt* d_gsn = nullptr;
-  F9* d_gsn9 = nullptr;                // the giant table in 9 x 29 limbs (x, y, p - x), for the F9 walk
   AffPt* d_offs = nullptr;
   uint32_t n_offs = 0, gpl = 0;
   AffPt* d_gofs = nullptr;             // per-group offsets expanded from gpl > 1 lane offsets
@@ -181,7 +180,7 @@ void free_slot(Slot& S);
 // empty (and the caller may go on with the slots it has).
 int ensure_slot_alloc(khb_ctx* c, Slot& S) {
   KHB_TRY(c, hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
-  KHB_TRY(c, hipMalloc(&S.d_scratch, (KHB_F9WALK ? sizeof(F9) : sizeof(Fe)) * kScratchEntries * c->lanes));
+  KHB_TRY(c, hipMalloc(&S.d_scratch, sizeof(Fe) * kScratchEntries * c->lanes));
   KHB_TRY(c, hipMalloc(&S.d_cand, sizeof(khb_cand) * kCandCap));
   KHB_TRY(c, hipMalloc(&S.d_degen, sizeof(khb_degenerate) * kDegenCap));
   KHB_TRY(c, hipMalloc(&S.d_counters, kCounterBytes));
@@ -253,7 +252,6 @@ ScanArgs make_args(khb_ctx* c, const Slot& S, uint32_t n_jobs, uint32_t group_be
   A.gate1 = c->d_gate1;
   A.gate1_mask = c->gate1_mask;
   A.gsn = c->d_gsn;
-  A.gsn9 = c->d_gsn9;
   A.offs = c->d_offs;
   A.gofs = c->gpl == 1 ? c->d_offs : c->d_gofs;
   A.centres = S.d_centres;
@@ -426,7 +424,6 @@ int khb_close(khb_ctx* c) {
   hipFree(c->d_gate);
   hipFree(c->d_gate1);
   hipFree(c->d_gsn);
-  hipFree(c->d_gsn9);
   hipFree(c->d_offs);
   hipFree(c->d_gofs);
   hipFree(c->d_abloom);
@@ -499,16 +496,6 @@ int khb_load_giant_table(khb_ctx* c, const uint8_t* gsn) {
   for (int i = 0; i < KHB_GIANT_TABLE; ++i) fe_sub(h.nx[i], zero, h.pt[i].x);
   if (!c->d_gsn) KHB_TRY(c, hipMalloc(&c->d_gsn, sizeof(h)));
   KHB_TRY(c, hipMemcpy(c->d_gsn, &h, sizeof(h), hipMemcpyHostToDevice));
-#if KHB_F9WALK
-  std::vector<F9> h9(3 * KHB_GIANT_TABLE);     // the table in 9 x 29 limbs for the F9 walk (scan_f9.hpp)
-  for (int i = 0; i < KHB_GIANT_TABLE; ++i) {
-    f9_from_fe(h9[i], h.pt[i].x);
-    f9_from_fe(h9[KHB_GIANT_TABLE + i], h.pt[i].y);
-    f9_from_fe(h9[2 * KHB_GIANT_TABLE + i], h.nx[i]);
-  }
-  if (!c->d_gsn9) KHB_TRY(c, hipMalloc(&c->d_gsn9, sizeof(F9) * h9.size()));
-  KHB_TRY(c, hipMemcpy(c->d_gsn9, h9.data(), sizeof(F9) * h9.size(), hipMemcpyHostToDevice));
-#endif
   c->gofs_stale = true;
   return KHB_OK;
 }
@@ -610,7 +597,7 @@ int khb_dump_x(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint32_t
     ScanArgs A = make_args(c, S, 1, group_begin, group_count, kBatch);
     A.xdump = d_x;
     const uint32_t blocks = (uint32_t)((A.n_items + kBlock - 1) / kBlock);
-    launch_bsgs(KHB_F9WALK ? kDumpG : kDump, blocks < c->lanes / kBlock ? blocks : c->lanes / kBlock, S.stream, A);
+    launch_bsgs(kDump, blocks < c->lanes / kBlock ? blocks : c->lanes / kBlock, S.stream, A);
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipStreamSynchronize(S.stream);

@@ -17,7 +17,6 @@
 #include "../../include/khbsgs.h"
 #include "device/fe.hpp"
 #include "device/fe_asm.hpp"
-#include "device/fe29.hpp"
 #include "device/bloom_probe.hpp"
 #include "device/hash160.hpp"
 
@@ -55,21 +54,12 @@ enum : int {
   kBaby = 6,       // baby-step table build: bloom_add of every x into L1/L2/L3 + bPtable records
   kScanG = 7,      // -m bsgs with a level-0 gate (the product path: walk_group_g)
   kScanG1 = 8,     // kScanG with the gate's stage-1 fold in front (khb_set_gate_stage1; k >= 4)
-  kDumpG = 9,      // -m bsgs parity of the product walk: kScanG's 9 x 29-bit arithmetic, every x written
 };
 constexpr bool is_gated(int m) { return m == kScanG || m == kScanG1; }
-#ifndef KHB_F9WALK
-// 1: the gated scan in 9 x 29-bit limbs (walk_group_g9, scan_f9.hpp; `make variants` only).  Fewer
-// VALU instructions than the 8 x 32 walk but slower on MI355X in every form tried: 2-4.6 % at 3 and 4
-// waves/SIMD, with a lower shader clock (profiles/r02_f9_walk.md, r03c_f9_ab.txt,
-// r03_calibration/f9_w3_ab.txt), so the product keeps the 8 x 32 walk_group_g.
-#define KHB_F9WALK 0
-#endif
-constexpr bool is_f9(int m) { return (KHB_F9WALK && is_gated(m)) || m == kDumpG; }   // walk in 9 x 29 limbs (fe29.hpp)
 constexpr bool is_scan(int m) { return m == kScan || is_gated(m); }
 constexpr bool is_addr(int m) { return m >= kAddrU && m <= kAddrDump; }
 constexpr bool needs_y(int m) { return m == kAddrU || m == kAddrB || m == kAddrDump; }
-constexpr bool is_dump(int m) { return m == kDump || m == kAddrDump || m == kBaby || m == kDumpG; }
+constexpr bool is_dump(int m) { return m == kDump || m == kAddrDump || m == kBaby; }
 #ifndef KHB_ADDR_WAVES_PER_SIMD
 #define KHB_ADDR_WAVES_PER_SIMD KHB_WAVES_PER_SIMD   // occupancy target of the -m address hash kernels
 #endif
@@ -91,7 +81,6 @@ struct ScanArgs {
   const uint8_t* __restrict__ bloom;
   BloomGeom geom;
   const AffPt* __restrict__ gsn;       // [0..511] GSn, [512] _2GSn
-  const F9* __restrict__ gsn9;         // the same in 9 x 29 limbs: 513 x, 513 y, then 513 (p - x)
   const AffPt* __restrict__ offs;      // lane start offsets
   const AffPt* __restrict__ gofs;      // per-group centre offsets j*_2GSn (scan_batch)
   const AffPt* __restrict__ centres;   // per-job group-0 centre
@@ -153,10 +142,8 @@ constexpr uint32_t kWavesPerBlock = kBlock / 64;
 
 // The count lives in LDS, not in a register: lanes of a wave may diverge (the ragged last lane of
 // a job, the tail of the item loop), and a register copy would go stale in the inactive lanes.
-typedef volatile __attribute__((address_space(3))) uint32_t* LdsWords;
 struct ProbeQueue {
   uint32_t* q;            // this wave's LDS region: kQWords arrays of kQCap words
-  LdsWords cn;            // F9 walk: this wave's p - C.x and C.y of the current group, [limb][lane]
   // this wave's queued-entry count, typed as an LDS pointer: through a generic (flat) pointer
   // every count access was a flat_load/flat_store, which counts against vmcnt AND lgkmcnt and
   // made each one wait for all outstanding vector-memory operations (the prefetched prefix).
@@ -868,10 +855,6 @@ __device__ __forceinline__ uint32_t scan_batch(const ScanArgs& A, ProbeQueue& Q,
   return walked;
 }
 
-#if KHB_F9WALK
-#include "scan_f9.hpp"        // the gated walk in 9 x 29-bit limbs (alternative build, `make variants`)
-#endif
-
 // Groups walked by the launch: a wave sum of every lane's count, one 64-bit atomic per wave into
 // counters[4..5].  The host compares it with n_jobs x group_count (khb_collect: KHB_EINCOMPLETE), so
 // a work-item handout that skipped or repeated a group cannot go unnoticed.  Called with the wave
@@ -900,16 +883,13 @@ template <int MODE>
 __global__ __launch_bounds__(kBlock, waves_per_simd(MODE)) void k_giant_scan(ScanArgs A) {
   clock_probe(A.counters, 0);
   constexpr bool QUEUE = is_scan(MODE);
-  constexpr bool BATCH = is_scan(MODE) || MODE == kDump || MODE == kDumpG;
+  constexpr bool BATCH = is_scan(MODE) || MODE == kDump;
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   Fe* scr = A.scratch + lane;
   __shared__ uint32_t s_queue[QUEUE ? kWavesPerBlock : 1][QUEUE ? kQWords * kQCap : 1];
   __shared__ uint32_t s_count[kWavesPerBlock];
-  // F9 walk: the group's p - C.x and C.y per lane in LDS (walk_group_g9), not in 18 VGPRs
-  __shared__ uint32_t s_cn[is_f9(MODE) ? kWavesPerBlock : 1][is_f9(MODE) ? 18 * 64 : 1];
   const uint32_t wave = QUEUE ? threadIdx.x >> 6 : 0;
-  ProbeQueue Q{s_queue[wave], (LdsWords)s_cn[is_f9(MODE) ? wave : 0],
-               (volatile __attribute__((address_space(3))) uint32_t*)&s_count[wave]};
+  ProbeQueue Q{s_queue[wave], (volatile __attribute__((address_space(3))) uint32_t*)&s_count[wave]};
   if (QUEUE) *Q.n = 0;
   uint32_t walked = 0;     // groups this lane walked (count_walked: the host checks the launch's total)
   if constexpr (BATCH) {
@@ -929,12 +909,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(MODE)) void k_giant_scan(Sca
         const uint32_t m = (uint32_t)(item % A.lanes_per_job);
         const uint32_t g0 = A.group_begin + m * kBatch;
         const uint32_t g1 = min(g0 + kBatch, A.group_end);
-#if KHB_F9WALK
-        if constexpr (is_f9(MODE))
-          walked += scan_batch9<MODE>(A, Q, job, g0, g1, lane);
-        else
-#endif
-          walked += scan_batch<MODE>(A, Q, job, g0, g1, scr);
+        walked += scan_batch<MODE>(A, Q, job, g0, g1, scr);
       }
     }
   } else {
@@ -968,7 +943,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(MODE)) void k_giant_scan(Sca
 }
 
 // Launchers of the k_giant_scan instances (one translation unit each, see above).
-void launch_bsgs(int mode, uint32_t blocks, hipStream_t stream, const ScanArgs& A);   // kScan, kScanG, kScanG1, kDumpG
+void launch_bsgs(int mode, uint32_t blocks, hipStream_t stream, const ScanArgs& A);   // kScan, kScanG, kScanG1, kDump
 void launch_addr(int mode, uint32_t blocks, hipStream_t stream, const ScanArgs& A);   // kAddrU, kAddrC, kAddrB, kAddrDump
 void launch_baby(uint32_t blocks, hipStream_t stream, const ScanArgs& A);             // kBaby
 

@@ -37,3 +37,15 @@ def blocks_fit(lo: int, hi: int, two_n: int, world: int, chunks_per_rank: int, k
         s, e = key_block(lo, hi, two_n, r, world, key)
         out.append((s, e, s + chunks_per_rank * two_n <= e))
     return out
+
+
+def fit_batch(lo: int, hi: int, two_n: int, world: int, steps: int, chunks: int, fill: int,
+              key: int | None = None) -> int:
+    """Chunks per step for `steps` steps (warmup + timed) of every rank inside its block: `chunks` when it
+    fits, else the largest multiple of `fill` (chunks that give every lane one work item) that does;
+    0 when not even one item per lane fits."""
+    blocks = blocks_fit(lo, hi, two_n, world, steps * chunks, key)
+    if all(ok for _, _, ok in blocks):
+        return chunks
+    room = min((e - s) // two_n for s, e, _ in blocks) // max(1, steps)
+    return (room // fill) * fill if room >= fill else 0

@@ -1,0 +1,83 @@
+"""bench.py --gpus N launches N ranks by itself: the launch decision, the spawned
+world (gloo on CPU, no GPU touched: --launch-check) and the failure paths."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from keyhuntm1cpu_amd import launch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _clean_env(**kw):
+    e = {k: v for k, v in os.environ.items()
+         if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "KHB_BENCH_CHILD")}
+    e.update(kw)
+    return e
+
+
+def test_plan():
+    assert launch.plan(1, {}) == "single"
+    assert launch.plan(8, {}) == "spawn"                       # bare --gpus 8: N children
+    assert launch.plan(8, {"WORLD_SIZE": ""}) == "spawn"
+    assert launch.plan(8, {"WORLD_SIZE": "8"}) == "rank"       # under torch.distributed.run
+    assert launch.plan(1, {"WORLD_SIZE": "1"}) == "single"
+    for gpus, ws in ((2, "8"), (8, "1"), (1, "2")):
+        with pytest.raises(SystemExit) as e:
+            launch.plan(gpus, {"WORLD_SIZE": ws})
+        assert e.value.code == 2
+    with pytest.raises(SystemExit):
+        launch.plan(0, {})
+    with pytest.raises(SystemExit):
+        launch.plan(2, {"WORLD_SIZE": "two"})
+
+
+def test_rank_env():
+    e = launch.rank_env({"X": "1"}, 3, 8, 12345)
+    assert (e["RANK"], e["LOCAL_RANK"], e["WORLD_SIZE"], e["MASTER_ADDR"], e["MASTER_PORT"], e["X"]) == \
+        ("3", "3", "8", "127.0.0.1", "12345", "1")
+
+
+def _bench(args, env, timeout=180):
+    return subprocess.run([sys.executable, BENCH, *args], env=env, capture_output=True, text=True, timeout=timeout,
+                          cwd="/tmp")
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bare_gpus_n_spawns_n_ranks(n):
+    r = _bench(["--gpus", str(n), "--launch-check"], _clean_env())
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1                                     # exactly rank 0's line on stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n
+    assert [v["rank"] for v in d["ranks"]] == list(range(n))
+    assert [v["local_rank"] for v in d["ranks"]] == list(range(n))
+    assert len({v["pid"] for v in d["ranks"]}) == n            # n distinct processes
+
+
+def test_single_gpu_runs_in_process():
+    r = _bench(["--gpus", "1", "--launch-check"], _clean_env())
+    assert r.returncode == 0, r.stderr
+    assert json.loads(r.stdout)["n_gpus"] == 1
+    assert "starting" not in r.stderr
+
+
+def test_world_size_mismatch_refused():
+    r = _bench(["--gpus", "4", "--launch-check"], _clean_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode == 2
+    assert r.stdout.strip() == ""
+    assert "differs from --gpus 4" in r.stderr
+
+
+def test_failing_rank_fails_the_launch():
+    r = _bench(["--gpus", "3", "--launch-check", "--launch-check-fail", "2"], _clean_env())
+    assert r.returncode == 3
+    assert r.stdout.strip() == ""                              # no line when a rank failed
+    assert "rank 2 exited with status 3" in r.stderr

@@ -36,10 +36,3 @@ def test_device_math_headers_on_host(tmp_path):
 def test_hash160_header_on_host(tmp_path):
     out = _build_and_run("test_hash160_host.cpp", tmp_path)
     assert "ok" in out
-
-
-def test_fe29_header_on_host(tmp_path):
-    """device/fe29.hpp (9 x 29-bit limbs of the -m bsgs walk) vs the oracle's exact field, incl. limbs
-    at the stated bounds and the gate words' rare-flag edge."""
-    out = _build_and_run("test_fe29_host.cpp", tmp_path)
-    assert out.startswith("ok")

@@ -88,3 +88,22 @@ def test_p66_blocks_overrun_detected():
     for world in (2, 4, 8):
         assert not all(ok for _, _, ok in blocks_fit(LO, HI, TWO_N, world, 105 * 4096, P66_KEY))
     assert all(ok for _, _, ok in blocks_fit(LO, HI, TWO_N, 1, 105 * 4096, P66_KEY))
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_p66_batch_shrinks_to_fit(world):
+    """bench.py's auto batch for a long run: shrunk to whole work items per lane so that every rank's
+    W + K steps stay inside its -b 66 block; unchanged when it fits; refused (0) below one item per lane."""
+    from keyhuntm1cpu_amd.partition import blocks_fit, fit_batch
+    fill = 384                                     # 196,608 lanes x 8 groups / 4096 groups per chunk
+    assert fit_batch(LO, HI, TWO_N, world, 25, 8 * fill, fill, P66_KEY) == 8 * fill
+    for steps in (105, 300):
+        c = fit_batch(LO, HI, TWO_N, world, steps, 8 * fill, fill, P66_KEY)
+        if c:
+            assert c % fill == 0 and fill <= c <= 8 * fill
+            assert all(ok for _, _, ok in blocks_fit(LO, HI, TWO_N, world, steps * c, P66_KEY))
+            if c < 8 * fill:
+                assert not all(ok for _, _, ok in blocks_fit(LO, HI, TWO_N, world, steps * (c + fill), P66_KEY))
+        else:
+            assert not all(ok for _, _, ok in blocks_fit(LO, HI, TWO_N, world, steps * fill, P66_KEY))
+    assert fit_batch(LO, HI, TWO_N, world, 5000, 8 * fill, fill, P66_KEY) == 0

@@ -42,26 +42,41 @@ if int(os.environ.get("GATE_ZERO", "0") or 0):
     lz = int(os.environ["GATE_ZERO"])
     gates[-lz] = bytes((1 << lz) // 8)
     gsets.append(-lz)
-engines = {}
-for p in paths:
-    for g in gsets:
-        e = Engine(0, lib_path=p)
-        e.load_bloom(bf, nb, bits, h)
-        if g:
-            e.load_gate(gates[g], abs(g), t.gate_probes())
-        e.load_giant_table(gsn)
-        e.load_lane_offsets(offs, gpl)
-        e.scan(centres[:64 * 8], 0, 64)
-        name = os.path.basename(p) + (f" +gate{g}" if g > 0 else f" +zerogate{-g}" if g else "")
-        engines[name] = (e, g)
-        print(f"{name}: lanes {e.lanes()}", flush=True)
-times = {n: [] for n in engines}
-mhz = {n: [] for n in engines}
+# One Engine at a time: each owns ~26 GB of scratch per submission slot, so every (variant, gate) pair
+# gets its own context per round, opened, timed and closed before the next one (round 3 kept all of them
+# open at once and ran out of HBM with six variants, gpurun_out/r03m/ab.txt).
+configs = [(p, g) for p in paths for g in gsets]
+
+
+def cfg_name(p, g):
+    return os.path.basename(p) + (f" +gate{g}" if g > 0 else f" +zerogate{-g}" if g else "")
+
+
+def open_engine(p, g):
+    e = Engine(0, lib_path=p)
+    e.load_bloom(bf, nb, bits, h)
+    if g:
+        e.load_gate(gates[g], abs(g), t.gate_probes())
+    e.load_giant_table(gsn)
+    e.load_lane_offsets(offs, gpl)
+    e.scan(centres[:64 * 8], 0, 64)               # warm: code object load, first-touch of the tables
+    return e
+
+
+times = {cfg_name(p, g): [] for p, g in configs}
+mhz = {n: [] for n in times}
 ncand = {}
 ref = {}
 for rnd in range(int(os.environ.get("ROUNDS", "3"))):
-    for n, (e, g) in engines.items():
-        c, d, st = e.scan(centres, 0, t.cycles)
+    for p, g in configs:
+        n = cfg_name(p, g)
+        e = open_engine(p, g)
+        try:
+            if rnd == 0:
+                print(f"{n}: lanes {e.lanes()}", flush=True)
+            c, d, st = e.scan(centres, 0, t.cycles)
+        finally:
+            e.close()
         times[n].append(st.kernel_ms)
         mhz[n].append(getattr(st, "shader_mhz", 0.0))
         ncand[n] = len(c)
@@ -76,7 +91,7 @@ for rnd in range(int(os.environ.get("ROUNDS", "3"))):
 for g in ref:   # a gate keeps a subset of the L1 candidates
     assert 0 not in ref or set(ref[g]) <= set(ref[0])
 steps = jobs * t.cycles * 1024
-for n in engines:
+for n in times:
     med = statistics.median(times[n])
     print(f"{n:34s} median {med:8.2f} ms  min {min(times[n]):8.2f}  {steps / med / 1e6:8.3f} G steps/s"
           f"  cand {ncand[n]}  clock {statistics.median(mhz[n]):7.1f} MHz", flush=True)
