@@ -41,6 +41,12 @@ extern "C" {
 #define KHB_GROUP 1024         /* giant steps per group: CPU_GRP_SIZE, keyhunt.cpp:127 */
 #define KHB_GIANT_TABLE 513    /* GSn[0..511] + _2GSn, keyhunt.cpp:1318-1338 */
 
+/* ABI version of this header (entry points, khb_stats and the other structs); bumped whenever one of
+ * them changes.  A binding checks khb_abi_version() == the KHB_ABI_VERSION it was written for before
+ * any other call (khb_stats gained launch_begin_ms/launch_end_ms/shader_mhz in ABI 3 and 4). */
+#define KHB_ABI_VERSION 4
+int khb_abi_version(void);
+
 typedef struct khb_ctx khb_ctx;
 
 /* One level-1 bloom hit: giant step `a` (= group*1024 + t, keyhunt.cpp:3948) of job `job`. */
@@ -88,8 +94,8 @@ uint32_t khb_default_lanes(int device);
  * consecutive groups of one job with two field inversions in total, so a launch fills the device
  * when n_jobs * ceil(group_count / khb_groups_per_item()) >= khb_lanes(ctx). */
 uint32_t khb_groups_per_item(void);
-/* Allocate the device state of the first `depth` submission slots now (1 or 2; the second slot's
- * prefix scratch is ~35 GB on MI355X) instead of on the first queued submission.  KHB_ENOMEM leaves the
+/* Allocate the device state of the first `depth` submission slots now (1 or 2; a slot's prefix scratch
+ * is 4,120 x 32 B x khb_lanes(ctx): ~26 GB at the auto 196,608 lanes on MI355X) instead of on the first queued submission.  KHB_ENOMEM leaves the
  * extra slot empty and the context usable with one submission in flight (the caller's queue depth 1). */
 int khb_reserve_slots(khb_ctx* ctx, int depth);
 /* Candidate ring entries a -m bsgs launch keeps (default and maximum 2^20).  Lowering it is for tests
@@ -113,7 +119,8 @@ int khb_load_bloom(khb_ctx* ctx, const uint8_t* bf_concat, uint64_t bytes_per_su
  * blocked bloom filter of 2^log2_bits bits in 64-bit blocks (block i = bytes 8i..8i+7, bit b of
  * the block = bit b%8 of byte 8i + b/8).  With x the canonical x-coordinate as an integer,
  * w0 = x mod 2^32 and w1 = (x >> 32) mod 2^32, x selects block w0 mod 2^(log2_bits-6) and within
- * it bits (w1 >> 6p) mod 64, p < probes; every baby-step x of the level-1 set has its bits set
+ * it, for p < probes, bit 32 (p mod 2) + ((w1 >> 5p) mod 32) (probes 0 and 2 in the block's low
+ * word, probe 1 in its high word); every baby-step x of the level-1 set has its bits set
  * (khb_build_baby writes one).  With a gate, the giant-step probe reads x's block (one 8-byte
  * load) and runs the level-1 check (both XXH64, all bits) only when all its bits are set: every
  * level-1 candidate that passes the gate is still reported, so no baby-step hit is lost.

@@ -17,6 +17,11 @@
 extern "C" {
 #endif
 
+/* ABI version of this header; bumped whenever a signature, a struct or an output array changes.
+ * A binding checks khh_abi_version() == the KHH_ABI_VERSION it was written for before any other call. */
+#define KHH_ABI_VERSION 4
+int khh_abi_version(void);
+
 typedef struct khh_tables khh_tables;
 
 /* Geometry + all tables.  n_str: -n value ("0x.." or decimal) or NULL (2^44); k: -k factor;
@@ -69,16 +74,21 @@ int khh_search(const khh_tables* t, const uint8_t* targets_xy, int n_targets, co
                char* err, size_t errlen);
 
 /* Persistent multi-GPU session: contexts opened and tables resident in HBM once, then any number
- * of searches.  stats_out of khh_session_run (9 entries): as khh_search, [6]=launches rescanned in
- * parts after a candidate-ring overflow, [7]=device-busy microseconds (union of each device's launch
- * intervals, summed over devices; two launches in flight overlap, so [7] <= [4]), [8]=average shader clock
- * of the launches in kHz (9 entries in all). */
+ * of searches.  khh_session_run writes the 6 stats entries of khh_search (stats_out holds 6).
+ * khh_session_run_ex writes the first min(stats_len, KHH_SESSION_STATS) of: those 6, [6]=launches
+ * rescanned in parts after a candidate-ring overflow, [7]=device-busy microseconds (union of each
+ * device's launch intervals, summed over devices; two launches in flight overlap, so [7] <= [4]),
+ * [8]=average shader clock of the launches in kHz. */
+#define KHH_SESSION_STATS 9
 typedef struct khh_session khh_session;
 khh_session* khh_session_open(const khh_tables* t, const int* devices, int n_devices, uint32_t lanes,
                               uint32_t chunks_per_batch, int check_threads, char* err, size_t errlen);
 int khh_session_run(khh_session* s, const uint8_t* targets_xy, int n_targets, const uint8_t start_be[32],
                     const uint8_t end_be[32], uint64_t max_chunks, int random_chunks, int* found, uint8_t* keys_be,
                     uint64_t* stats_out, char* err, size_t errlen);
+int khh_session_run_ex(khh_session* s, const uint8_t* targets_xy, int n_targets, const uint8_t start_be[32],
+                       const uint8_t end_be[32], uint64_t max_chunks, int random_chunks, int* found, uint8_t* keys_be,
+                       uint64_t* stats_out, uint32_t stats_len, char* err, size_t errlen);
 void khh_session_close(khh_session* s);
 /* Test hooks: candidate ring capacity per launch (0 = default 2^20; small values drive the
  * split-and-rescan path), the level-0 gate on/off, recording of every level-1 candidate of the next
@@ -107,13 +117,19 @@ void khh_addr_giant_table(const khh_addr* a, uint8_t out[513 * 64]);
 uint32_t khh_addr_lane_offsets(const khh_addr* a, uint8_t* out /* n*64, may be NULL */, uint32_t* gpl);
 /* Sequential (random_chunks = 0) or -R search of [start, end) with search 0/1/2 (-l).  Found keys
  * (32 B BE each) with compressed flags and rmd160s, in discovery order; *n_found may exceed cap.
- * stats_out (nullable, 8): [0]=chunks [1]=keys [2]=bloom hits [3]=degenerate groups [4]=kernel us
- * [5]=launches [6]=average shader clock of the launches in kHz [7]=rescans (launches whose bloom hits
- * overflowed khb_addr_hit_capacity and were rescanned in parts). */
+ * stats_out (nullable): [0]=chunks [1]=keys [2]=bloom hits [3]=degenerate groups [4]=kernel us
+ * [5]=launches; khh_addr_search writes these 6.  khh_addr_search_ex writes the first
+ * min(stats_len, KHH_ADDR_STATS) of them and [6]=average shader clock of the launches in kHz,
+ * [7]=rescans (launches whose bloom hits overflowed khb_addr_hit_capacity and were rescanned in parts). */
+#define KHH_ADDR_STATS 8
 int khh_addr_search(const khh_addr* a, const uint8_t start_be[32], const uint8_t end_be[32], int search,
                     int random_chunks, const int* devices, int n_devices, uint32_t lanes, uint64_t max_chunks,
                     uint8_t* keys_be, uint8_t* compressed, uint8_t* rmd, uint32_t cap, uint32_t* n_found,
                     uint64_t* stats_out, char* err, size_t errlen);
+int khh_addr_search_ex(const khh_addr* a, const uint8_t start_be[32], const uint8_t end_be[32], int search,
+                       int random_chunks, const int* devices, int n_devices, uint32_t lanes, uint64_t max_chunks,
+                       uint8_t* keys_be, uint8_t* compressed, uint8_t* rmd, uint32_t cap, uint32_t* n_found,
+                       uint64_t* stats_out, uint32_t stats_len, char* err, size_t errlen);
 /* Tests: bloom-hit ring capacity of the search's launches (0 = the library default, 2^18). */
 int khh_addr_set_hit_capacity(khh_addr* a, uint32_t cap);
 /* hash160 of a public key (x||y BE) and its P2PKH address (out_addr >= 36 bytes) */

@@ -306,14 +306,14 @@ bool Tables::build(const Geometry& g, int nthreads, uint32_t groups_per_lane, st
           if (need_l2 && ic < g.m2) l2[idx].add32_atomic(xb);
           if (need_l1 && ic < to) {
             l1[idx].add32_atomic(xb);
-            // blocked gate (khb_load_gate): block w0 mod 2^(gate_log2-6), bits (w1 >> 6p) mod 64;
+            // blocked gate (khb_load_gate): block w0 mod 2^(gate_log2-6), bit (w1 >> 5p) mod 32 of word p mod 2;
             // w0 = x mod 2^32 is big-endian bytes 28..31, w1 = (x >> 32) mod 2^32 bytes 24..27
             if (gate_probes) {
               const uint32_t w0 = ((uint32_t)xb[28] << 24) | ((uint32_t)xb[29] << 16) | ((uint32_t)xb[30] << 8) | xb[31];
               const uint32_t w1 = ((uint32_t)xb[24] << 24) | ((uint32_t)xb[25] << 16) | ((uint32_t)xb[26] << 8) | xb[27];
               const uint64_t blk = w0 & (uint32_t)((1ull << (gate_log2 - 6)) - 1);
               for (uint32_t p = 0; p < gate_probes; ++p) {
-                const uint32_t b = (w1 >> (6 * p)) & 63u;
+                const uint32_t b = 32u * (p & 1u) + ((w1 >> (5 * p)) & 31u);
                 __atomic_fetch_or(&gate[8 * blk + (b >> 3)], (uint8_t)(1u << (b & 7)), __ATOMIC_RELAXED);
               }
             }

@@ -33,6 +33,8 @@ static void set_err(char* err, size_t n, const std::string& m) {
 
 extern "C" {
 
+int khh_abi_version(void) { return KHH_ABI_VERSION; }
+
 khh_tables* khh_tables_new(const char* n_str, int k, int threads, uint32_t gpl, char* err, size_t errlen) {
   Geometry g;
   std::string e;
@@ -203,6 +205,13 @@ void khh_session_close(khh_session* s) { delete s; }
 int khh_session_run(khh_session* s, const uint8_t* targets_xy, int n_targets, const uint8_t start_be[32],
                     const uint8_t end_be[32], uint64_t max_chunks, int random_chunks, int* found, uint8_t* keys_be,
                     uint64_t* stats_out, char* err, size_t errlen) {
+  return khh_session_run_ex(s, targets_xy, n_targets, start_be, end_be, max_chunks, random_chunks, found, keys_be,
+                            stats_out, stats_out ? 6 : 0, err, errlen);
+}
+
+int khh_session_run_ex(khh_session* s, const uint8_t* targets_xy, int n_targets, const uint8_t start_be[32],
+                       const uint8_t end_be[32], uint64_t max_chunks, int random_chunks, int* found, uint8_t* keys_be,
+                       uint64_t* stats_out, uint32_t stats_len, char* err, size_t errlen) {
   if (!s || !targets_xy || n_targets <= 0) return KHB_EINVAL;
   std::vector<Target> tg((size_t)n_targets);
   for (int k = 0; k < n_targets; ++k) tg[k].p = pt_from_be(targets_xy + 64 * k);
@@ -221,15 +230,11 @@ int khh_session_run(khh_session* s, const uint8_t* targets_xy, int n_targets, co
     if (keys_be) (f.empty() ? U256() : keys[k]).to_be(keys_be + 32 * k);
   }
   if (stats_out) {
-    stats_out[0] = st.chunks;
-    stats_out[1] = st.giant_steps;
-    stats_out[2] = st.candidates;
-    stats_out[3] = st.degenerate;
-    stats_out[4] = (uint64_t)(st.kernel_seconds * 1e6);
-    stats_out[5] = st.launches;
-    stats_out[6] = st.rescans;
-    stats_out[7] = (uint64_t)(st.busy_seconds * 1e6);
-    stats_out[8] = st.shader_mhz_n ? (uint64_t)(1e3 * st.shader_mhz_sum / st.shader_mhz_n) : 0;
+    const uint64_t v[KHH_SESSION_STATS] = {
+        st.chunks, st.giant_steps, st.candidates, st.degenerate, (uint64_t)(st.kernel_seconds * 1e6), st.launches,
+        st.rescans, (uint64_t)(st.busy_seconds * 1e6),
+        st.shader_mhz_n ? (uint64_t)(1e3 * st.shader_mhz_sum / st.shader_mhz_n) : 0};
+    memcpy(stats_out, v, sizeof(uint64_t) * (stats_len < KHH_SESSION_STATS ? stats_len : KHH_SESSION_STATS));
   }
   if (rc) set_err(err, errlen, e);
   return rc;
@@ -258,10 +263,8 @@ int khh_search(const khh_tables* t, const uint8_t* targets_xy, int n_targets, co
                char* err, size_t errlen) {
   khh_session* s = khh_session_open(t, devices, n_devices, lanes, chunks_per_batch, 0, err, errlen);
   if (!s) return KHB_ENODEV;
-  uint64_t st8[9] = {0};
-  int rc = khh_session_run(s, targets_xy, n_targets, start_be, end_be, max_chunks, 0, found, keys_be, st8, err,
-                           errlen);
-  if (stats_out) memcpy(stats_out, st8, 6 * sizeof(uint64_t));   // khh_search's stats hold 6
+  int rc = khh_session_run(s, targets_xy, n_targets, start_be, end_be, max_chunks, 0, found, keys_be, stats_out, err,
+                           errlen);                                 // khh_search's stats hold 6
   khh_session_close(s);
   return rc;
 }
@@ -339,6 +342,14 @@ int khh_addr_search(const khh_addr* a, const uint8_t start_be[32], const uint8_t
                     int random_chunks, const int* devices, int n_devices, uint32_t lanes, uint64_t max_chunks,
                     uint8_t* keys_be, uint8_t* compressed, uint8_t* rmd, uint32_t cap, uint32_t* n_found,
                     uint64_t* stats_out, char* err, size_t errlen) {
+  return khh_addr_search_ex(a, start_be, end_be, search, random_chunks, devices, n_devices, lanes, max_chunks, keys_be,
+                            compressed, rmd, cap, n_found, stats_out, stats_out ? 6 : 0, err, errlen);
+}
+
+int khh_addr_search_ex(const khh_addr* a, const uint8_t start_be[32], const uint8_t end_be[32], int search,
+                       int random_chunks, const int* devices, int n_devices, uint32_t lanes, uint64_t max_chunks,
+                       uint8_t* keys_be, uint8_t* compressed, uint8_t* rmd, uint32_t cap, uint32_t* n_found,
+                       uint64_t* stats_out, uint32_t stats_len, char* err, size_t errlen) {
   if (!a || !start_be || !end_be || search < 0 || search > 2) return KHB_EINVAL;
   AddrConfig cfg;
   cfg.search = search;
@@ -368,14 +379,10 @@ int khh_addr_search(const khh_addr* a, const uint8_t start_be[32], const uint8_t
   const int rc = addr_search(a->T, a->G, cfg, cb, &st, &e);
   if (n_found) *n_found = nf;
   if (stats_out) {
-    stats_out[0] = st.chunks;
-    stats_out[1] = st.keys;
-    stats_out[2] = st.hits;
-    stats_out[3] = st.degenerate;
-    stats_out[4] = (uint64_t)(st.kernel_seconds * 1e6);
-    stats_out[5] = st.launches;
-    stats_out[6] = st.shader_mhz_n ? (uint64_t)(1e3 * st.shader_mhz_sum / st.shader_mhz_n) : 0;
-    stats_out[7] = st.rescans;
+    const uint64_t v[KHH_ADDR_STATS] = {
+        st.chunks, st.keys, st.hits, st.degenerate, (uint64_t)(st.kernel_seconds * 1e6), st.launches,
+        st.shader_mhz_n ? (uint64_t)(1e3 * st.shader_mhz_sum / st.shader_mhz_n) : 0, st.rescans};
+    memcpy(stats_out, v, sizeof(uint64_t) * (stats_len < KHH_ADDR_STATS ? stats_len : KHH_ADDR_STATS));
   }
   if (rc) set_err(err, errlen, e);
   return rc;

@@ -8,6 +8,7 @@
 #include <new>
 #include <vector>
 #include "scan_kernels.hpp"
+#include <utility>
 
 using namespace khbk;
 
@@ -139,7 +140,17 @@ struct khb_ctx {
   int head = 0;                        // oldest in-flight slot
   int queued = 0;                      // submissions in flight (0..kQueueDepth)
   uint32_t cand_cap = kCandCap;        // candidate ring entries a launch may fill (khb_set_candidate_capacity)
-  hipEvent_t epoch = nullptr;          // time origin of khb_stats.launch_begin_ms / launch_end_ms (khb_reset_epoch)
+  // The context's clock (khb_stats.launch_begin_ms / launch_end_ms; khb_reset_epoch restarts it): the
+  // `epoch` event sits epoch_ms after the clock's origin.  hipEventElapsedTime is a float, so the anchor
+  // moves forward once its distance to a launch passes kReanchorMs (a float ms keeps ~4 us at 60 s, but
+  // ~1 ms after 4.6 h): begin = epoch_ms + elapsed(epoch, ev0) in double, end = begin + the launch's own
+  // elapsed(ev0, ev1) (the busy-time union no longer drifts on long CLI runs).
+  // The previous anchor stays valid as a fallback for a launch of the other slot that began before the
+  // current anchor was recorded (a negative distance).
+  hipEvent_t epoch = nullptr;
+  hipEvent_t epoch_prev = nullptr;
+  double epoch_ms = 0.0, epoch_prev_ms = 0.0;
+  bool have_prev = false;
   // -m address
   uint8_t* d_abloom = nullptr;
   BloomGeom ageom{};
@@ -273,20 +284,37 @@ ScanArgs make_args(khb_ctx* c, const Slot& S, uint32_t n_jobs, uint32_t group_be
 
 // kernel_ms and the launch's interval on the context's clock (khb_reset_epoch), from the slot's events;
 // the shader clock from the kernel's clock_probe samples.
-void launch_times(const khb_ctx* c, const Slot& S, khb_stats* st) {
+// Called after S's stream has drained (the slot's launch is complete and the stream idle).
+constexpr float kReanchorMs = 60000.f;
+void launch_times(khb_ctx* c, const Slot& S, khb_stats* st) {
   uint64_t p[4];
   memcpy(p, S.h_counters + 8, sizeof p);
   st->shader_mhz = (p[3] > p[1] && p[2] > p[0]) ? (float)(100.0 * (double)(p[2] - p[0]) / (double)(p[3] - p[1])) : 0.f;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, S.ev0, S.ev1) != hipSuccess) ms = -1.f;
   st->kernel_ms = ms;
-  float b = -1.f, e = -1.f;
-  if (c->epoch && hipEventElapsedTime(&b, c->epoch, S.ev0) == hipSuccess &&
-      hipEventElapsedTime(&e, c->epoch, S.ev1) == hipSuccess) {
-    st->launch_begin_ms = b;
-    st->launch_end_ms = e;
+  float b = -1.f, bp = -1.f;
+  double begin = -1.0;
+  const bool cur = c->epoch && hipEventElapsedTime(&b, c->epoch, S.ev0) == hipSuccess && b >= 0.f;
+  if (cur)
+    begin = c->epoch_ms + (double)b;
+  else if (c->have_prev && hipEventElapsedTime(&bp, c->epoch_prev, S.ev0) == hipSuccess && bp >= 0.f)
+    begin = c->epoch_prev_ms + (double)bp;
+  if (begin >= 0.0 && ms >= 0.f) {
+    st->launch_begin_ms = begin;
+    st->launch_end_ms = begin + (double)ms;
   } else {
     st->launch_begin_ms = st->launch_end_ms = -1.0;
+  }
+  float d = 0.f;
+  if (cur && b > kReanchorMs && c->epoch_prev && hipEventRecord(c->epoch_prev, S.stream) == hipSuccess &&
+      hipEventSynchronize(c->epoch_prev) == hipSuccess &&
+      hipEventElapsedTime(&d, c->epoch, c->epoch_prev) == hipSuccess) {
+    // the new anchor (recorded now on the idle stream) becomes current; the old one the fallback
+    std::swap(c->epoch, c->epoch_prev);
+    c->epoch_prev_ms = c->epoch_ms;
+    c->epoch_ms += (double)d;
+    c->have_prev = true;
   }
 }
 
@@ -338,6 +366,8 @@ const char* khb_strerror(int code) {
 int khb_last_hip_error(const khb_ctx* c) { return c ? c->last_hip : 0; }
 void* khb_stream(khb_ctx* c) { return c ? (void*)c->slot[0].stream : nullptr; }
 uint32_t khb_lanes(const khb_ctx* c) { return c ? c->lanes : 0; }
+int khb_abi_version(void) { return KHB_ABI_VERSION; }
+
 uint32_t khb_groups_per_item(void) { return kBatch; }
 
 int khb_reserve_slots(khb_ctx* c, int depth) {
@@ -369,6 +399,8 @@ int khb_reset_epoch(khb_ctx* c) {
   if (c->queued) return KHB_EBUSY;
   KHB_TRY(c, hipSetDevice(c->device));
   KHB_TRY(c, hipEventRecord(c->epoch, c->slot[0].stream));
+  c->epoch_ms = c->epoch_prev_ms = 0.0;
+  c->have_prev = false;
   return KHB_OK;
 }
 
@@ -405,7 +437,8 @@ int khb_open(int device, uint32_t lanes, khb_ctx** out) {
   c->lanes = lanes;
   hipError_t e = hipSetDevice(device);
   int rc = e == hipSuccess ? ensure_slot(c, c->slot[0]) : hip_fail(c, e);
-  if (!rc && (e = hipEventCreate(&c->epoch)) == hipSuccess) e = hipEventRecord(c->epoch, c->slot[0].stream);
+  if (!rc && (e = hipEventCreate(&c->epoch)) == hipSuccess && (e = hipEventCreate(&c->epoch_prev)) == hipSuccess)
+    e = hipEventRecord(c->epoch, c->slot[0].stream);
   if (!rc && e != hipSuccess) rc = hip_fail(c, e);
   if (rc) {
     khb_close(c);
@@ -420,6 +453,7 @@ int khb_close(khb_ctx* c) {
   if (c->device >= 0) hipSetDevice(c->device);
   for (Slot& S : c->slot) free_slot(S);
   if (c->epoch) hipEventDestroy(c->epoch);
+  if (c->epoch_prev) hipEventDestroy(c->epoch_prev);
   hipFree(c->d_bloom);
   hipFree(c->d_gate);
   hipFree(c->d_gate1);

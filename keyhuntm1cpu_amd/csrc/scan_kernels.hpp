@@ -101,8 +101,8 @@ struct ScanArgs {
   uint64_t blimit[3];                  // ic < blimit[l] goes into level l (l1ext, m2, m3)
   uint32_t* __restrict__ bp;           // m3 x 16-byte struct bsgs_xvalue records (null = skipped)
   // level-0 gate (khb_load_gate): a blocked bloom of (gate_mask + 1) 64-bit blocks; x selects
-  // block x.v[0] & gate_mask and bits (x.v[1] >> 6p) & 63, p < gate_probes, in it, all set for
-  // every x of the L1 set; null = no gate.  kBaby writes it (gate_w, ic < glimit).
+  // block x.v[0] & gate_mask and in it bit (x.v[1] >> 5p) & 31 of word p & 1, p < gate_probes, all
+  // set for every x of the L1 set; null = no gate.  kBaby writes it (gate_w, ic < glimit).
   const uint8_t* __restrict__ gate;
   uint32_t* __restrict__ gate_w;
   uint32_t gate_probes;
@@ -202,37 +202,32 @@ __device__ __forceinline__ void q_push(ProbeQueue& Q, bool hit, const Fe& x, uin
   *Q.n = n + (uint32_t)__popcll(m);
 }
 
-// The gate's bit positions in x's block: (x.v[1] >> 6p) & 63 for p < probes, packed 6 bits each
-// into three slots (unused probes repeat the last used one, so every test checks three bits).
-__device__ __forceinline__ uint32_t gate_bits(const ScanArgs& A, const Fe& x) {
-  const uint32_t w = x.v[1];
-  const uint32_t b0 = w & 63u, b1 = A.gate_probes > 1 ? (w >> 6) & 63u : b0;
-  const uint32_t b2 = A.gate_probes > 2 ? (w >> 12) & 63u : b1;
-  return b0 | (b1 << 6) | (b2 << 12);
+// The gate's bits in x's 64-bit block (lo, hi words): probe p tests bit (w1 >> 5p) mod 32 of word p mod 2
+// (p = 0: lo, 1: hi, 2: lo), w1 = x.v[1].  32-bit shifts take their amount mod 32 in hardware, so each
+// probe is one shift of a block word with no word select: the round-3 layout (6-bit positions in the
+// whole block) selected the word per probe with a v_cndmask_b32 on VCC.  Probes
+// beyond A.gate_probes are masked to "set" by wave-uniform words (no per-lane select either).
+struct GateMask {
+  uint32_t m1, m2;       // 1 when probe 1 / probe 2 is unused
+};
+__device__ __forceinline__ GateMask gate_mask(const ScanArgs& A) {
+  return GateMask{A.gate_probes < 2 ? 1u : 0u, A.gate_probes < 3 ? 1u : 0u};
 }
-
-// All three packed bits set in the 64-bit block (lo, hi)?  (One 64-bit shift per bit instead of the
-// word select measured no faster, profiles/r02p_gate_shr64_ab.txt.)
-__device__ __forceinline__ bool gate_block_pass(uint32_t lo, uint32_t hi, uint32_t bits) {
-  uint32_t r = 1u;
-#pragma unroll
-  for (int p = 0; p < 3; ++p) {
-    const uint32_t b = (bits >> (6 * p)) & 63u;
-    r &= ((b & 32u) ? hi : lo) >> (b & 31u);
-  }
+__device__ __forceinline__ bool gate_block_pass(uint32_t lo, uint32_t hi, uint32_t w1, GateMask m) {
+  const uint32_t r = (lo >> (w1 & 31u)) & ((hi >> ((w1 >> 5) & 31u)) | m.m1) & ((lo >> ((w1 >> 10) & 31u)) | m.m2);
   return r & 1u;
 }
 
-// A gate test: x's 64-bit block of the map (one 8-byte load: a single cache line per x whatever
-// the probe count) and the packed bit positions.
+// A gate test: x's 64-bit block of the map (one 8-byte load: a single cache line per x whatever the
+// probe count) and x's second word, which holds the bit positions.
 struct GatePend {
-  uint32_t lo, hi, bits;
-  __device__ __forceinline__ bool pass() const { return gate_block_pass(lo, hi, bits); }
+  uint32_t lo, hi, w1;
+  __device__ __forceinline__ bool pass(GateMask m) const { return gate_block_pass(lo, hi, w1, m); }
 };
 
 __device__ __forceinline__ GatePend gate_issue(const ScanArgs& A, const Fe& x) {
   const uint2 w = reinterpret_cast<const uint2*>(A.gate)[x.v[0] & A.gate_mask];
-  return GatePend{w.x, w.y, gate_bits(A, x)};
+  return GatePend{w.x, w.y, x.v[1]};
 }
 
 // kScanG: gate test of one walk step's two x (x2 absent at step 511: has2 = false, uniform).  Both
@@ -241,22 +236,22 @@ template <bool STAGE1>
 __device__ __forceinline__ void gate_pair(const ScanArgs& A, ProbeQueue& Q, const Fe& x1, uint32_t step1, bool has2,
                                           const Fe& x2, uint32_t step2, uint32_t job) {
   bool h1, h2;
+  const GateMask gm = gate_mask(A);
   if constexpr (STAGE1) {
     // stage 1 (L2-resident fold); the full gate's line is fetched only for its survivors
-    const uint32_t b1 = gate_bits(A, x1), b2 = gate_bits(A, x2);
     const uint2 f1 = reinterpret_cast<const uint2*>(A.gate1)[x1.v[0] & A.gate1_mask];
     const uint2 f2 = reinterpret_cast<const uint2*>(A.gate1)[x2.v[0] & A.gate1_mask];
-    const bool s1 = gate_block_pass(f1.x, f1.y, b1), s2 = has2 && gate_block_pass(f2.x, f2.y, b2);
+    const bool s1 = gate_block_pass(f1.x, f1.y, x1.v[1], gm), s2 = has2 && gate_block_pass(f2.x, f2.y, x2.v[1], gm);
     if (__ballot(s1 || s2) == 0) return;
     uint2 w1 = make_uint2(0u, 0u), w2 = make_uint2(0u, 0u);
     if (s1) w1 = reinterpret_cast<const uint2*>(A.gate)[x1.v[0] & A.gate_mask];
     if (s2) w2 = reinterpret_cast<const uint2*>(A.gate)[x2.v[0] & A.gate_mask];
-    h1 = s1 && gate_block_pass(w1.x, w1.y, b1);
-    h2 = s2 && gate_block_pass(w2.x, w2.y, b2);
+    h1 = s1 && gate_block_pass(w1.x, w1.y, x1.v[1], gm);
+    h2 = s2 && gate_block_pass(w2.x, w2.y, x2.v[1], gm);
   } else {
     const GatePend q1 = gate_issue(A, x1), q2 = gate_issue(A, x2);
-    h1 = q1.pass();
-    h2 = has2 && q2.pass();
+    h1 = q1.pass(gm);
+    h2 = has2 && q2.pass(gm);
   }
   if (__ballot(h1 || h2) == 0) return;
   q_push(Q, h1, x1, job, step1);
@@ -270,7 +265,7 @@ __device__ __forceinline__ bool first_bit(const ScanArgs& A, const Fe& x, uint64
   if (A.gate) {
     a = 0;
     const uint2 w = reinterpret_cast<const uint2*>(A.gate)[x.v[0] & A.gate_mask];
-    return gate_block_pass(w.x, w.y, gate_bits(A, x));
+    return gate_block_pass(w.x, w.y, x.v[1], gate_mask(A));
   }
   uint64_t w[4];
   x_words(w, x);
@@ -393,10 +388,8 @@ __device__ __forceinline__ void baby_point(const ScanArgs& A, const Fe& x, uint3
   const uint64_t a = xxh64_32(w, KHB_BLOOM_SEED);
   if (A.gate_w && ic < A.glimit) {
     const uint32_t blk = x.v[0] & A.gate_mask;
-    for (uint32_t p = 0; p < A.gate_probes; ++p) {
-      const uint32_t b = (x.v[1] >> (6 * p)) & 63u;
-      atomicOr(A.gate_w + 2 * blk + (b >> 5), 1u << (b & 31));
-    }
+    for (uint32_t p = 0; p < A.gate_probes; ++p)      // gate_block_pass: bit (w1 >> 5p) mod 32 of word p mod 2
+      atomicOr(A.gate_w + 2 * blk + (p & 1u), 1u << ((x.v[1] >> (5 * p)) & 31u));
   }
   const uint64_t b = xxh64_32(w, a);
   const uint32_t sub = x.v[7] >> 24;

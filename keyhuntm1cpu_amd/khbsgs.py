@@ -38,6 +38,7 @@ class Stats(C.Structure):
 
 
 _libs: dict[str, C.CDLL] = {}
+KHB_ABI_VERSION = 4
 
 
 def lib(path: str | None = None) -> C.CDLL:
@@ -48,6 +49,14 @@ def lib(path: str | None = None) -> C.CDLL:
             raise KhbError(f"{path} not built: run `make` (or __graft_entry__.build())")
         L = C.CDLL(path)
         P = C.POINTER
+        # include/khbsgs.h KHB_ABI_VERSION: the structs and signatures below are written for it (older
+        # timing-only variant builds without the symbol are accepted for tools/perf_variants.py)
+        if hasattr(L, "khb_abi_version"):
+            v = L.khb_abi_version()
+            if v != KHB_ABI_VERSION:
+                raise KhbError(f"{path}: ABI {v}, this binding is written for {KHB_ABI_VERSION}: rebuild (`make`)")
+        elif path == LIB_PATH:
+            raise KhbError(f"{path} predates khb_abi_version: rebuild (`make`)")
         L.khb_device_count.argtypes = [P(C.c_int)]
         L.khb_open.argtypes = [C.c_int, C.c_uint32, P(C.c_void_p)]
         L.khb_close.argtypes = [C.c_void_p]

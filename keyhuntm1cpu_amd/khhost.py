@@ -12,6 +12,10 @@ LIB_PATH = os.path.join(LIB_DIR, "libkhhost.so")
 _lib = None
 
 
+KHH_ABI_VERSION = 4                 # include/khhost.h
+KHH_SESSION_STATS, KHH_ADDR_STATS = 9, 8
+
+
 class KhhError(RuntimeError):
     pass
 
@@ -23,6 +27,9 @@ def lib() -> C.CDLL:
             raise KhhError(f"{LIB_PATH} not built: run `make`")
         L = C.CDLL(LIB_PATH)
         P = C.POINTER
+        v = L.khh_abi_version() if hasattr(L, "khh_abi_version") else 0
+        if v != KHH_ABI_VERSION:        # include/khhost.h KHH_ABI_VERSION
+            raise KhhError(f"{LIB_PATH}: ABI {v}, this binding is written for {KHH_ABI_VERSION}: rebuild (`make`)")
         L.khh_tables_new.restype = C.c_void_p
         L.khh_tables_new.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_uint32, C.c_char_p, C.c_size_t]
         L.khh_tables_free.argtypes = [C.c_void_p]
@@ -57,6 +64,9 @@ def lib() -> C.CDLL:
                                        C.c_size_t]
         L.khh_session_run.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, C.c_uint64, C.c_int,
                                       P(C.c_int), C.c_char_p, P(C.c_uint64), C.c_char_p, C.c_size_t]
+        L.khh_session_run_ex.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, C.c_uint64,
+                                         C.c_int, P(C.c_int), C.c_char_p, P(C.c_uint64), C.c_uint32, C.c_char_p,
+                                         C.c_size_t]
         L.khh_session_close.argtypes = [C.c_void_p]
         L.khh_session_set_test_hooks.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_char_p]
         L.khh_session_recorded.restype = C.c_uint64
@@ -77,6 +87,9 @@ def lib() -> C.CDLL:
         L.khh_addr_search.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int, C.c_int, P(C.c_int), C.c_int,
                                       C.c_uint32, C.c_uint64, C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint32,
                                       P(C.c_uint32), P(C.c_uint64), C.c_char_p, C.c_size_t]
+        L.khh_addr_search_ex.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int, C.c_int, P(C.c_int), C.c_int,
+                                         C.c_uint32, C.c_uint64, C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint32,
+                                         P(C.c_uint32), P(C.c_uint64), C.c_uint32, C.c_char_p, C.c_size_t]
         L.khh_addr_set_hit_capacity.argtypes = [C.c_void_p, C.c_uint32]
         L.khh_hash160.argtypes = [C.c_char_p, C.c_int, C.c_char_p]
         L.khh_rmd_to_address.argtypes = [C.c_char_p, C.c_char_p]
@@ -258,10 +271,10 @@ class Session:
         n = len(targets_xy)
         found = (C.c_int * n)()
         keys = C.create_string_buffer(32 * n)
-        stats = (C.c_uint64 * 9)()
+        stats = (C.c_uint64 * KHH_SESSION_STATS)()
         err = C.create_string_buffer(256)
-        rc = lib().khh_session_run(self.h, b"".join(targets_xy), n, _b32(start), _b32(end), max_chunks,
-                                   1 if random_chunks else 0, found, keys, stats, err, 256)
+        rc = lib().khh_session_run_ex(self.h, b"".join(targets_xy), n, _b32(start), _b32(end), max_chunks,
+                                      1 if random_chunks else 0, found, keys, stats, KHH_SESSION_STATS, err, 256)
         if rc:
             raise KhhError(f"search failed ({rc}): {err.value.decode()}")
         res = [int.from_bytes(keys.raw[32 * i:32 * i + 32], "big") if found[i] else None for i in range(n)]
@@ -364,11 +377,12 @@ class Addr:
         comp = C.create_string_buffer(cap)
         rmd = C.create_string_buffer(20 * cap)
         nf = C.c_uint32(0)
-        st = (C.c_uint64 * 8)()
+        st = (C.c_uint64 * KHH_ADDR_STATS)()
         devs = (C.c_int * len(devices))(*devices)
         err = C.create_string_buffer(256)
-        rc = lib().khh_addr_search(self.h, _b32(start), _b32(end), search, 1 if random_chunks else 0, devs,
-                                   len(devices), lanes, max_chunks, keys, comp, rmd, cap, C.byref(nf), st, err, 256)
+        rc = lib().khh_addr_search_ex(self.h, _b32(start), _b32(end), search, 1 if random_chunks else 0, devs,
+                                      len(devices), lanes, max_chunks, keys, comp, rmd, cap, C.byref(nf), st,
+                                      KHH_ADDR_STATS, err, 256)
         if rc:
             raise KhhError(f"khh_addr_search: {err.value.decode()} [{rc}]")
         n = min(nf.value, cap)

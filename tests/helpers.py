@@ -33,10 +33,11 @@ def rand_fe(rng: random.Random) -> int:
 
 def gate_bits(lg: int, probes: int, x: int) -> list[int]:
     """Bit indices of the level-0 gate (khb_load_gate) for x: a blocked bloom of 64-bit blocks,
-    block (x mod 2^32) mod 2^(lg-6), bits ((x >> 32) mod 2^32 >> 6p) mod 64 within it, p < probes."""
+    block (x mod 2^32) mod 2^(lg-6); within it, for p < probes, bit ((x >> 32) mod 2^32 >> 5p) mod 32
+    of 32-bit word p mod 2 (include/khbsgs.h)."""
     blk = (x & 0xFFFFFFFF) & ((1 << (lg - 6)) - 1)
     w1 = (x >> 32) & 0xFFFFFFFF
-    return [64 * blk + ((w1 >> (6 * p)) & 63) for p in range(probes)]
+    return [64 * blk + 32 * (p & 1) + ((w1 >> (5 * p)) & 31) for p in range(probes)]
 
 
 def gate_pass(gate: bytes, lg: int, probes: int, x: int) -> bool:

@@ -58,3 +58,30 @@ def test_null_context_is_einval():
     lib.khb_load_gate.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32]
     assert lib.khb_set_gate_stage1(None, 25) == -1
     assert lib.khb_load_gate(None, None, 0, 1) == -1
+
+
+def _header_define(header: str, name: str) -> int:
+    src = open(os.path.join(REPO_DIR, "include", header)).read()
+    return int(re.search(r"#define\s+" + name + r"\s+(\d+)", src).group(1))
+
+
+def test_abi_versions_match_headers_and_bindings():
+    """The libraries report the ABI version their headers declare, and the Python bindings are written
+    for that version (they refuse a library of another one)."""
+    from keyhuntm1cpu_amd import khbsgs, khhost
+    b = C.CDLL(os.path.join(LIB_DIR, "libkhbsgs.so"))
+    h = C.CDLL(os.path.join(LIB_DIR, "libkhhost.so"))
+    assert b.khb_abi_version() == _header_define("khbsgs.h", "KHB_ABI_VERSION") == khbsgs.KHB_ABI_VERSION
+    assert h.khh_abi_version() == _header_define("khhost.h", "KHH_ABI_VERSION") == khhost.KHH_ABI_VERSION
+    assert _header_define("khhost.h", "KHH_SESSION_STATS") == khhost.KHH_SESSION_STATS
+    assert _header_define("khhost.h", "KHH_ADDR_STATS") == khhost.KHH_ADDR_STATS
+    khbsgs.lib()
+    khhost.lib()
+
+
+def test_khb_stats_layout():
+    """khb_stats as the binding reads it (include/khbsgs.h, ABI 4)."""
+    from keyhuntm1cpu_amd.khbsgs import Stats
+    assert [f for f, _ in Stats._fields_] == ["n_cand", "n_degenerate", "giant_steps", "kernel_ms", "launch_begin_ms",
+                                             "launch_end_ms", "shader_mhz"]
+    assert C.sizeof(Stats) == 48

@@ -80,8 +80,9 @@ for rnd in range(int(os.environ.get("ROUNDS", "3"))):
         times[n].append(st.kernel_ms)
         mhz[n].append(getattr(st, "shader_mhz", 0.0))
         ncand[n] = len(c)
-        if "_p" in n.split()[0] or "nonop" in n or "_rm" in n or "_scr" in n:   # timing-only experiments: not comparable
-            continue
+        timing_only = [v for v in os.environ.get("TIMING_ONLY", "").split(",") if v]
+        if "_p" in n.split()[0] or "nonop" in n or "_rm" in n or "_scr" in n or any(v in n for v in timing_only):
+            continue                               # timing-only experiments: candidates not comparable
         s = sorted(c)
         if g < 0:                                  # the zero gate: nothing passes
             assert not s, f"{n}: a zero gate passed candidates"
