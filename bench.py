@@ -430,12 +430,20 @@ def main():
 
 
 # -m address (configs[4]).  Executed VALU lane-instructions per key at -l both: PMC SQ_INSTS_VALU x 64 / keys
-# of one 8-chunk launch (profiles/r02w/addr_valu_counter_collection.csv, 4.968e12 x 64 / 2^35).  The
+# of one 8-chunk launch (tools/addr_floor.py under rocprofv3; profiles/r04b/addr_libkhbsgs: 4.9695e12 x 64 /
+# 2^35 = 9,256.1; round 2's profiles/r02w/addr_valu_counter_collection.csv read 9,253.4).  The
 # issue ceiling is that of the kernel's own instruction mix: the hash blocks are 43 % full-rate VALU
 # (v_add_u32, v_bitop3_b32, shifts: ~2.6 SIMD cycles per wave-instruction at 4 waves/SIMD) and 57 %
 # half-rate (v_alignbit_b32, v_add3_u32, v_mad_u64_u32: ~4.6), profiles/r03_valu_cost.txt and
 # tools/debug/bb_path.py over tools/microbench/hash_isa.hip = 3.73 cycles per wave-instruction.
-ADDR_EXEC_VALU_PER_KEY = {2: 9253.4}
+ADDR_EXEC_VALU_PER_KEY = {2: 9256.1}
+# The VALU floor per key of -l both, in the same unit: the hash blocks as compiled alone
+# (tools/microbench/hash_isa.hip -> profiles/r02_hash_isa_counts.txt: the 02/03 compressed hash160 pair
+# 4,401, the uncompressed hash160 3,616, XXH64 of three 20-byte hashes 3 x 137 / 2) plus the x/y walk,
+# measured as PMC SQ_INSTS_VALU of the hash-less build of the same kernel (tools/experiments/addrwalk_patch.py;
+# profiles/r04b/addr_libkhbsgs_addrwalk: 5.308e11 x 64 / 2^35 = 988.7 per key).
+ADDR_FLOOR_TERMS = {2: {"hash160_compressed_pair": 4401, "hash160_uncompressed": 3616, "xxh64_x3": 205.5,
+                        "xy_walk": 988.7}}
 ADDR_MIX_CYCLES_PER_INSTR = 3.73
 ADDR_ALG_OPS = {0: 2 * 2032 + 1440 + 680, 1: 2 * (2032 + 1440) + 530, 2: 4 * 2032 + 3 * 1440 + 680}
 
@@ -526,7 +534,14 @@ def bench_address(args, world, rank, dist, torch):
                          "peak_basis": "the hash mix's issue ceiling, %.2f SIMD cycles per wave-instruction (43 %% "
                                        "full-rate / 57 %% half-rate VALU, profiles/r03_valu_cost.txt) x 1024 SIMDs at "
                                        "the launches' measured shader clock" % ADDR_MIX_CYCLES_PER_INSTR,
-                         "executed_source": "profiles/r02w/addr_valu_counter_collection.csv (PMC SQ_INSTS_VALU)"})
+                         "executed_source": "profiles/r04b/addr_libkhbsgs (PMC SQ_INSTS_VALU, tools/addr_floor.py)"})
+        fl = ADDR_FLOOR_TERMS.get(args.search)
+        if fl:
+            floor = sum(fl.values())
+            roofline.update({"floor_valu_lane_instr_per_key": round(floor, 1), "floor_terms": fl,
+                             "executed_over_floor": round(e / floor, 4),
+                             "floor_basis": "hash blocks compiled alone (profiles/r02_hash_isa_counts.txt) + the x/y "
+                                            "walk's PMC count in the hash-less build (profiles/r04b)"})
     roofline["algorithmic_ops_per_key"] = ADDR_ALG_OPS[args.search]
     roofline["traffic"] = None
     cpu = None

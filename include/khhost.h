@@ -117,6 +117,10 @@ void khh_addr_giant_table(const khh_addr* a, uint8_t out[513 * 64]);
 uint32_t khh_addr_lane_offsets(const khh_addr* a, uint8_t* out /* n*64, may be NULL */, uint32_t* gpl);
 /* Sequential (random_chunks = 0) or -R search of [start, end) with search 0/1/2 (-l).  Found keys
  * (32 B BE each) with compressed flags and rmd160s, in discovery order; *n_found may exceed cap.
+ * Discovery order is batch order, and (chunk, key) order inside a batch, except after an overflow: a batch
+ * whose bloom hits overflowed khb_addr_hit_capacity is rescanned in parts queued behind the batch already
+ * submitted after it, so its keys are reported after that later batch's (the bsgs session reorders its
+ * candidates the same way).  Callers that need range order sort the keys.
  * stats_out (nullable): [0]=chunks [1]=keys [2]=bloom hits [3]=degenerate groups [4]=kernel us
  * [5]=launches; khh_addr_search writes these 6.  khh_addr_search_ex writes the first
  * min(stats_len, KHH_ADDR_STATS) of them and [6]=average shader clock of the launches in kHz,
