@@ -43,8 +43,9 @@ extern "C" {
 
 /* ABI version of this header (entry points, khb_stats and the other structs); bumped whenever one of
  * them changes.  A binding checks khb_abi_version() == the KHB_ABI_VERSION it was written for before
- * any other call (khb_stats gained launch_begin_ms/launch_end_ms/shader_mhz in ABI 3 and 4). */
-#define KHB_ABI_VERSION 4
+ * any other call (khb_stats gained launch_begin_ms/launch_end_ms/shader_mhz in ABI 3 and 4; ABI 5 added
+ * khb_load_check_tables / khb_check). */
+#define KHB_ABI_VERSION 5
 int khb_abi_version(void);
 
 typedef struct khb_ctx khb_ctx;
@@ -158,6 +159,54 @@ int khb_collect(khb_ctx* ctx, khb_cand* cand, uint32_t cap, khb_degenerate* dege
  * that one, not this). */
 int khb_scan(khb_ctx* ctx, const uint8_t* centres_xy_be, uint32_t n_jobs, uint32_t group_begin,
              uint32_t group_count, khb_cand* cand, uint32_t cap, khb_stats* stats);
+
+/* ---- second / third check on the device ----
+ * bsgs_secondcheck + bsgs_thirdcheck (keyhunt.cpp:4271-4368) for a batch of level-1 candidates, one
+ * device lane each: base = start + a*BSGS_M_double, Q = target - base*G, the 32 points Q + BSGS_AMP2[i]
+ * into the level-2 bloom; for each hit i the third check on base + i*BSGS_M2_double with BSGS_AMP3, the
+ * level-3 bloom, bsgs_searchbinary over bPtable (3748-3773, its exact probe order) and the key
+ * verification by ComputePublicKey; calcualteindex (6680-6689).  It replaces the host loop the
+ * candidates feed at keyhunt.cpp:3947-3982; the found key equals the reference's.
+ * Tables are copied to the device by khb_load_check_tables: */
+typedef struct {
+  const uint8_t* gtable;            /* 32*256 points x||y BE, secp->GTable of Secp256K1::Init
+                                       (secp256k1/SECP256K1.cpp:43-54): entry 256*i + b - 1 = b * 2^(8i) * G,
+                                       b in 1..255 (entry 256*i + 255 is not read) */
+  const uint8_t* amp2;              /* BSGS_AMP2[0..31] x||y BE (keyhunt.cpp:1339-1350) */
+  const uint8_t* amp3;              /* BSGS_AMP3[0..31] x||y BE (keyhunt.cpp:1352-1363) */
+  const uint8_t* l2;                /* bloom_bPx2nd[0..255].bf concatenated (one geometry, as khb_load_bloom) */
+  uint64_t l2_bytes_per_sub, l2_bits_per_sub;
+  uint32_t l2_hashes;
+  const uint8_t* l3;                /* bloom_bPx3rd[0..255].bf concatenated */
+  uint64_t l3_bytes_per_sub, l3_bits_per_sub;
+  uint32_t l3_hashes;
+  const uint8_t* bptable;           /* bPtable: m3 x struct bsgs_xvalue (16 B: value[6], 2 pad, uint64 index LE),
+                                       sorted as bsgs_sort leaves it */
+  uint64_t m3;                      /* bsgs_m3 */
+  uint8_t m_double_be[32];          /* BSGS_M_double */
+  uint8_t m2_double_be[32];         /* BSGS_M2_double */
+  uint8_t m3_be[32];                /* BSGS_M3 */
+  uint8_t m3_double_be[32];         /* BSGS_M3_double */
+} khb_check_tables;
+int khb_load_check_tables(khb_ctx* ctx, const khb_check_tables* tables);
+
+typedef struct {
+  uint8_t start_be[32];             /* start_range of bsgs_secondcheck: the chunk's base (BSGS_CURRENT) */
+  uint32_t a;                       /* the candidate's giant step (khb_cand.a) */
+  uint32_t target;                  /* index into targets_xy */
+} khb_check_in;
+typedef struct {
+  uint8_t key_be[32];               /* the private key when found */
+  uint32_t found;                   /* bsgs_secondcheck's return value (0 or 1) */
+  uint32_t l2_hits;                 /* level-2 bloom hits (third checks run) */
+  uint32_t l3_hits;                 /* level-3 bloom hits in those third checks */
+  uint32_t bp_hits;                 /* bPtable matches (each verified by ComputePublicKey) */
+} khb_check_out;
+/* Synchronous; runs on the context's own check stream (high priority), so it may be called while scan
+ * submissions are in flight: its lanes take the CU slots the running launch's last waves free.
+ * targets_xy: n_targets points x||y BE (OriginalPointsBSGS).  KHB_ESTATE before khb_load_check_tables. */
+int khb_check(khb_ctx* ctx, const uint8_t* targets_xy, uint32_t n_targets, const khb_check_in* in, uint32_t n,
+              khb_check_out* out);
 
 /* ---- parity / debug ---- */
 /* x-coordinates (BE, probe order t = 0..1023 per group) of groups [group_begin,

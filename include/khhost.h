@@ -19,7 +19,7 @@ extern "C" {
 
 /* ABI version of this header; bumped whenever a signature, a struct or an output array changes.
  * A binding checks khh_abi_version() == the KHH_ABI_VERSION it was written for before any other call. */
-#define KHH_ABI_VERSION 4
+#define KHH_ABI_VERSION 5
 int khh_abi_version(void);
 
 typedef struct khh_tables khh_tables;
@@ -78,8 +78,9 @@ int khh_search(const khh_tables* t, const uint8_t* targets_xy, int n_targets, co
  * khh_session_run_ex writes the first min(stats_len, KHH_SESSION_STATS) of: those 6, [6]=launches
  * rescanned in parts after a candidate-ring overflow, [7]=device-busy microseconds (union of each
  * device's launch intervals, summed over devices; two launches in flight overlap, so [7] <= [4]),
- * [8]=average shader clock of the launches in kHz. */
-#define KHH_SESSION_STATS 9
+ * [8]=average shader clock of the launches in kHz, [9]=candidates confirmed on the GPU (khb_check),
+ * [10]=microseconds spent in those khb_check calls. */
+#define KHH_SESSION_STATS 11
 typedef struct khh_session khh_session;
 khh_session* khh_session_open(const khh_tables* t, const int* devices, int n_devices, uint32_t lanes,
                               uint32_t chunks_per_batch, int check_threads, char* err, size_t errlen);
@@ -95,6 +96,15 @@ void khh_session_close(khh_session* s);
  * runs (khh_session_recorded), and optionally a replacement level-1 bloom of the tables' geometry
  * (256 sub-blooms concatenated; NULL keeps the tables'). */
 int khh_session_set_test_hooks(khh_session* s, uint32_t cand_cap, int use_gate, int record, const uint8_t* l1_concat);
+/* Where later runs confirm their level-1 candidates (bsgs_secondcheck/thirdcheck, keyhunt.cpp:4271-4368):
+ * 0 = the host's CPU pool (default), 1 = the GPU that scanned them (khb_check; the check tables are
+ * loaded into every context), 2 = the GPU for batches of more than 4096 candidates, else the host. */
+#define KHH_CHECK_HOST 0
+#define KHH_CHECK_DEVICE 1
+#define KHH_CHECK_AUTO 2
+int khh_session_set_check_mode(khh_session* s, int mode);
+/* Secp256K1::Init's GTable (secp256k1/SECP256K1.cpp:43-54), 32*256 points x||y BE (khb_check_tables.gtable). */
+void khh_gtable(uint8_t out[32 * 256 * 64]);
 /* Candidates recorded in the last run: chunk base (32 B BE), target index, giant step a; returns the
  * count (may exceed cap). */
 uint64_t khh_session_recorded(const khh_session* s, uint8_t* bases_be, uint32_t* targets, uint32_t* a, uint64_t cap);

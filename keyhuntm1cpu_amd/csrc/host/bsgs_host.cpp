@@ -354,6 +354,19 @@ std::vector<uint8_t> Tables::l1_concat() const {
   return out;
 }
 
+std::vector<uint8_t> Tables::bloom_concat(int level) const {
+  const std::vector<BloomFilter>& L = level == 1 ? l1 : level == 2 ? l2 : l3;
+  std::vector<uint8_t> out(256 * L[0].bytes);
+  for (int i = 0; i < 256; ++i) memcpy(out.data() + i * L[0].bytes, L[i].bf.data(), L[0].bytes);
+  return out;
+}
+
+std::vector<uint8_t> Tables::amp_table_be(int level) const {
+  std::vector<uint8_t> out(32 * 64);
+  for (int i = 0; i < 32; ++i) pt_to_be(out.data() + 64 * i, level == 2 ? amp2[i] : amp3[i]);
+  return out;
+}
+
 std::vector<uint8_t> Tables::giant_table_be() const {
   std::vector<uint8_t> out(513 * 64);
   for (int i = 0; i < kHalf; ++i) pt_to_be(out.data() + 64 * i, gsn[i]);
@@ -457,13 +470,16 @@ void Tables::chunk_aux_run(const U256& base0, size_t n, Pt* aux, int threads) co
 }
 
 bool Tables::searchbinary(const uint8_t* x, uint64_t& idx) const {
-  // bsgs_searchbinary (keyhunt.cpp:3748-3773): probes bytes 16..21 of x
-  int64_t lo = 0, hi = (int64_t)bp.size() - 1;
-  while (lo <= hi) {
-    int64_t mid = lo + (hi - lo) / 2;
-    int r = memcmp(x + 16, bp[mid].value, 6);
-    if (r == 0) { idx = bp[mid].index; return true; }
-    if (r < 0) hi = mid - 1; else lo = mid + 1;
+  // bsgs_searchbinary (keyhunt.cpp:3748-3773), its own probe sequence (bytes 16..21 of x): with equal
+  // 6-byte keys in bPtable the entry it lands on, and so the key the third check tries, is the reference's
+  int64_t min = 0, max = (int64_t)bp.size(), half = max, current = 0;
+  while (half >= 1) {
+    half = (max - min) / 2;
+    const int r = memcmp(x + 16, bp[(size_t)(current + half)].value, 6);
+    if (r == 0) { idx = bp[(size_t)(current + half)].index; return true; }
+    if (r < 0) max = max - half;
+    else min = min + half;
+    current = min;
   }
   return false;
 }

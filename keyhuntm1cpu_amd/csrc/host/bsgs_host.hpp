@@ -77,6 +77,8 @@ struct Tables {
                   const std::function<void(const std::string&)>& log) const;
   static std::string file_name(const Geometry& g, uint32_t which);
   std::vector<uint8_t> l1_concat() const;
+  std::vector<uint8_t> bloom_concat(int level) const;    // level 1..3: 256 sub-blooms concatenated
+  std::vector<uint8_t> amp_table_be(int level) const;    // level 2, 3: BSGS_AMP2 / BSGS_AMP3, 32 x||y BE
   std::vector<uint8_t> giant_table_be() const;
   std::vector<uint8_t> lane_offsets_be() const;
 

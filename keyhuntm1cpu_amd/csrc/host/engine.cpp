@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <deque>
 #include <mutex>
 #include <thread>
@@ -48,6 +49,7 @@ struct Shared {
   std::vector<int>& found;
   std::vector<U256>& keys;
   SearchStats& stats;
+  std::vector<uint8_t> targets_xy;   // the targets x||y BE, for khb_check
   uint64_t claimed = 0;
   int n_found = 0;
   bool stop = false;
@@ -56,7 +58,9 @@ struct Shared {
 
   Shared(const Tables& t, const std::vector<Target>& tg, const SearchConfig& c, const SearchCallbacks& b,
          std::vector<int>& f, std::vector<U256>& k, SearchStats& s)
-      : T(t), targets(tg), cfg(c), cb(b), found(f), keys(k), stats(s) {}
+      : T(t), targets(tg), cfg(c), cb(b), found(f), keys(k), stats(s), targets_xy(64 * tg.size()) {
+    for (size_t i = 0; i < tg.size(); ++i) pt_to_be(targets_xy.data() + 64 * i, tg[i].p);
+  }
 };
 
 struct Batch {
@@ -190,9 +194,43 @@ void job_centres(const Tables& T, const std::vector<U256>& bases, const std::vec
 
 namespace {
 
+// The device check of a batch's candidates (khb_check): ok / key per candidate, as Tables::secondcheck.
+int confirm_device(Shared& S, khb_ctx* ctx, const Batch& b, const std::vector<khb_cand>& cands,
+                   const std::vector<int>& found_snapshot, std::vector<int>& ok, std::vector<U256>& key) {
+  std::vector<khb_check_in> in;
+  std::vector<size_t> idx;
+  in.reserve(cands.size());
+  for (size_t i = 0; i < cands.size(); ++i) {
+    const uint32_t job = cands[i].job;
+    const uint32_t k = b.job_target[job];
+    if (found_snapshot[k]) continue;
+    khb_check_in c{};
+    b.bases[b.job_chunk[job]].to_be(c.start_be);
+    c.a = cands[i].a;
+    c.target = k;
+    in.push_back(c);
+    idx.push_back(i);
+  }
+  if (in.empty()) return KHB_OK;
+  std::vector<khb_check_out> out(in.size());
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = khb_check(ctx, S.targets_xy.data(), (uint32_t)S.targets.size(), in.data(), (uint32_t)in.size(),
+                           out.data());
+  const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (rc) return rc;
+  for (size_t m = 0; m < in.size(); ++m) {
+    ok[idx[m]] = out[m].found ? 1 : 0;
+    if (out[m].found) key[idx[m]] = U256::from_be(out[m].key_be);
+  }
+  std::lock_guard<std::mutex> lk(S.mu);
+  S.stats.device_checked += in.size();
+  S.stats.device_check_seconds += dt;
+  return KHB_OK;
+}
+
 // Confirm level-1 candidates (bsgs_secondcheck, keyhunt.cpp:3947-3982): speculative parallel
-// checks, then in-order resolution.
-void confirm(Shared& S, const Batch& b, std::vector<khb_cand>& cands, int threads) {
+// checks (the CPU pool, or the device: SearchConfig::check_mode), then in-order resolution.
+int confirm(Shared& S, khb_ctx* ctx, const Batch& b, std::vector<khb_cand>& cands, int threads) {
   std::sort(cands.begin(), cands.end(), [](const khb_cand& x, const khb_cand& y) {
     return x.job != y.job ? x.job < y.job : x.a < y.a;
   });
@@ -203,12 +241,18 @@ void confirm(Shared& S, const Batch& b, std::vector<khb_cand>& cands, int thread
     std::lock_guard<std::mutex> lk(S.mu);
     found_snapshot = S.found;
   }
-  parallel_for(cands.size(), threads, [&](size_t i) {
-    const uint32_t job = cands[i].job;
-    const uint32_t k = b.job_target[job];
-    if (found_snapshot[k]) return;
-    ok[i] = S.T.secondcheck(b.bases[b.job_chunk[job]], cands[i].a, S.targets[k].p, key[i]) ? 1 : 0;
-  });
+  const bool dev = S.cfg.check_mode == kCheckDevice || (S.cfg.check_mode == kCheckAuto && cands.size() > kCheckAutoMin);
+  if (dev) {
+    const int rc = confirm_device(S, ctx, b, cands, found_snapshot, ok, key);
+    if (rc) return rc;
+  } else {
+    parallel_for(cands.size(), threads, [&](size_t i) {
+      const uint32_t job = cands[i].job;
+      const uint32_t k = b.job_target[job];
+      if (found_snapshot[k]) return;
+      ok[i] = S.T.secondcheck(b.bases[b.job_chunk[job]], cands[i].a, S.targets[k].p, key[i]) ? 1 : 0;
+    });
+  }
   std::lock_guard<std::mutex> lk(S.mu);
   for (size_t i = 0; i < cands.size(); ++i) {
     if (!ok[i]) continue;
@@ -220,6 +264,7 @@ void confirm(Shared& S, const Batch& b, std::vector<khb_cand>& cands, int thread
     if (S.cb.on_found) S.cb.on_found((int)k, key[i]);
   }
   if (S.n_found == (int)S.targets.size()) S.stop = true;   // "All points were found"
+  return KHB_OK;
 }
 
 uint32_t batch_chunks(const Tables& T, const SearchConfig& cfg, size_t ntargets, uint32_t ctx_lanes) {
@@ -363,7 +408,8 @@ void device_thread(Shared& S, khb_ctx* ctx) {
     }
     if (!overflow) {
       cands.assign(cbuf.begin(), cbuf.begin() + st.n_cand);
-      confirm(S, b, cands, threads);                           // overlaps the GPU scan of the queue
+      const int vrc = confirm(S, ctx, b, cands, threads);      // overlaps the GPU scan of the queue
+      if (vrc) { fail(vrc, "khb_check"); rc = vrc; continue; }
     }
     if (q.empty()) fill();     // rescan parts left after the last batch
   }
@@ -372,6 +418,30 @@ void device_thread(Shared& S, khb_ctx* ctx) {
 }
 
 }  // namespace
+
+int load_check_tables(khb_ctx* c, const Tables& T) {
+  const std::vector<uint8_t> l2 = T.bloom_concat(2), l3 = T.bloom_concat(3);
+  const std::vector<uint8_t> a2 = T.amp_table_be(2), a3 = T.amp_table_be(3);
+  khb_check_tables ct{};
+  ct.gtable = gtable_be().data();
+  ct.amp2 = a2.data();
+  ct.amp3 = a3.data();
+  ct.l2 = l2.data();
+  ct.l2_bytes_per_sub = T.l2[0].bytes;
+  ct.l2_bits_per_sub = T.l2[0].bits;
+  ct.l2_hashes = T.l2[0].hashes;
+  ct.l3 = l3.data();
+  ct.l3_bytes_per_sub = T.l3[0].bytes;
+  ct.l3_bits_per_sub = T.l3[0].bits;
+  ct.l3_hashes = T.l3[0].hashes;
+  ct.bptable = reinterpret_cast<const uint8_t*>(T.bp.data());
+  ct.m3 = T.bp.size();
+  T.geo.M_double.to_be(ct.m_double_be);
+  T.geo.M2_double.to_be(ct.m2_double_be);
+  T.geo.M3.to_be(ct.m3_be);
+  T.geo.M3_double.to_be(ct.m3_double_be);
+  return khb_load_check_tables(c, &ct);
+}
 
 int Session::open(const Tables& T, const SearchConfig& cfg, std::string& err) {
   close();
@@ -388,6 +458,7 @@ int Session::open(const Tables& T, const SearchConfig& cfg, std::string& err) {
     if (!rc) rc = khb_load_giant_table(c, gsn.data());
     if (!rc) rc = khb_load_lane_offsets(c, offs.data(), (uint32_t)T.lane_offs.size(), T.gpl);
     if (!rc && cfg.cand_cap) rc = khb_set_candidate_capacity(c, cfg.cand_cap);
+    if (!rc && cfg.check_mode != kCheckHost) rc = load_check_tables(c, T);
     if (rc) {
       err = "[E] GPU " + std::to_string(d) + ": " + khb_strerror(rc);
       if (c) khb_close(c);
@@ -411,6 +482,18 @@ int Session::set_test_hooks(uint32_t cand_cap, bool use_gate, const uint8_t* l1_
   }
   cfg_.cand_cap = cand_cap;
   cfg_.use_gate = use_gate;
+  return 0;
+}
+
+int Session::set_check_mode(int mode) {
+  if (!T_) return KHB_ESTATE;
+  if (mode < kCheckHost || mode > kCheckAuto) return KHB_EINVAL;
+  if (mode != kCheckHost && cfg_.check_mode == kCheckHost)
+    for (void* c : ctx_) {
+      const int rc = load_check_tables((khb_ctx*)c, *T_);
+      if (rc) return rc;
+    }
+  cfg_.check_mode = mode;
   return 0;
 }
 

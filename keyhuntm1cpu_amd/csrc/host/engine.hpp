@@ -14,6 +14,8 @@
 
 #include "bsgs_host.hpp"
 
+struct khb_ctx;
+
 namespace khb {
 
 struct Target {
@@ -38,7 +40,14 @@ struct SearchConfig {
   uint32_t cand_cap = 0;           // candidate ring entries per launch (0 = library default, 2^20); tests
                                    // lower it to drive the overflow path (split + rescan)
   bool record_candidates = false;  // tests: report every level-1 candidate (SearchCallbacks::on_candidate)
+  // Where the level-1 candidates are confirmed (bsgs_secondcheck/thirdcheck, keyhunt.cpp:4271-4368):
+  // kCheckHost on the CPU pool, kCheckDevice on the GPU that scanned them (khb_check), kCheckAuto on
+  // the GPU when a batch holds more than kCheckAutoMin candidates (the gated scan's ~30/s stay on the
+  // host, whose pool answers in microseconds; an ungated or dense-bloom scan moves to the device).
+  int check_mode = 0;
 };
+enum : int { kCheckHost = 0, kCheckDevice = 1, kCheckAuto = 2 };
+constexpr uint32_t kCheckAutoMin = 4096;
 
 struct SearchStats {
   uint64_t launches = 0;           // GPU scan launches (one per batch per device)
@@ -52,6 +61,8 @@ struct SearchStats {
                                    // device-busy time (two launches in flight overlap, so < kernel_seconds)
   double shader_mhz_sum = 0;       // sum of the launches' average shader clocks (khb_stats.shader_mhz)
   uint64_t shader_mhz_n = 0;
+  uint64_t device_checked = 0;     // candidates confirmed on the GPU (khb_check)
+  double device_check_seconds = 0; // wall time of those khb_check calls
 };
 
 struct SearchCallbacks {
@@ -83,12 +94,17 @@ class Session {
   // tests: candidate ring capacity per launch (0 = default), the level-0 gate on/off, and optionally
   // a replacement level-1 bloom of the same geometry (256 sub-blooms concatenated; null = the tables')
   int set_test_hooks(uint32_t cand_cap, bool use_gate, const uint8_t* l1_concat = nullptr);
+  // SearchConfig::check_mode for later runs; loads the device check tables when a device mode needs them.
+  int set_check_mode(int mode);
 
  private:
   const Tables* T_ = nullptr;
   SearchConfig cfg_;
   std::vector<void*> ctx_;   // khb_ctx*
 };
+
+// The check tables of T (level-2/3 blooms, bPtable, AMP2/AMP3, GTable, M constants) into a context.
+int load_check_tables(khb_ctx* c, const Tables& T);
 
 // Runs the search over [start, end) on a temporary session.  Returns 0, or a negative khbsgs error code.  found/keys are
 // sized to targets.size().  stats is updated live (read it from another thread for the

@@ -55,6 +55,8 @@ void menu() {
   printf("--gpu       use the GPU path (always on: keyhunt_amd has no CPU giant-step path)\n");
   printf("-g ids      GPU device ids, comma separated (default 0)\n");
   printf("--gpu-blocks n   persistent workgroups per GPU (256 lanes each)\n");
+  printf("--check where    confirm candidates (second/third check) on the host, the gpu, or auto (default host)\n");
+  printf("--no-gate   probe every giant step in the level-1 bloom (no level-0 gate; same keys, more candidates)\n");
   printf("\nExample:\n\n./keyhunt_amd -m bsgs -f tests/63.pub -b 63 -q -g 0\n\n");
   exit(EXIT_FAILURE);
 }
@@ -162,6 +164,8 @@ int main(int argc, char** argv) {
                                      {"gpu-blocks", required_argument, nullptr, 1002},
                                      {"max-chunks", required_argument, nullptr, 1003},
                                      {"cpu-build", no_argument, nullptr, 1004},
+                                     {"check", required_argument, nullptr, 1005},
+                                     {"no-gate", no_argument, nullptr, 1006},
                                      {nullptr, 0, nullptr, 0}};
   int c;
   while ((c = getopt_long(argc, argv, "deh6MqRSB:b:c:C:E:f:I:k:l:m:N:n:p:r:s:t:v:G:8:z:g:", longopts, nullptr)) != -1) {
@@ -259,6 +263,13 @@ int main(int argc, char** argv) {
       case 1002: gpu_blocks = (uint32_t)strtoul(optarg, nullptr, 10); break;
       case 1003: cfg.max_chunks = strtoull(optarg, nullptr, 10); break;
       case 1004: cpu_build = true; break;
+      case 1005:                                    // where candidates are confirmed (engine.hpp check_mode)
+        if (!strcmp(optarg, "host")) cfg.check_mode = kCheckHost;
+        else if (!strcmp(optarg, "gpu")) cfg.check_mode = kCheckDevice;
+        else if (!strcmp(optarg, "auto")) cfg.check_mode = kCheckAuto;
+        else { fprintf(stderr, "[E] --check: host, gpu or auto\n"); exit(EXIT_FAILURE); }
+        break;
+      case 1006: cfg.use_gate = false; break;       // the reference's exact level-1 candidate stream
       case 'C': case 'E': case 'N': case 'p': case 'v': case 'G': case '8': case 'z':
         break;   // options of the other search modes
       default:

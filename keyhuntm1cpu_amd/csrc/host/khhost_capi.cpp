@@ -233,7 +233,8 @@ int khh_session_run_ex(khh_session* s, const uint8_t* targets_xy, int n_targets,
     const uint64_t v[KHH_SESSION_STATS] = {
         st.chunks, st.giant_steps, st.candidates, st.degenerate, (uint64_t)(st.kernel_seconds * 1e6), st.launches,
         st.rescans, (uint64_t)(st.busy_seconds * 1e6),
-        st.shader_mhz_n ? (uint64_t)(1e3 * st.shader_mhz_sum / st.shader_mhz_n) : 0};
+        st.shader_mhz_n ? (uint64_t)(1e3 * st.shader_mhz_sum / st.shader_mhz_n) : 0, st.device_checked,
+        (uint64_t)(st.device_check_seconds * 1e6)};
     memcpy(stats_out, v, sizeof(uint64_t) * (stats_len < KHH_SESSION_STATS ? stats_len : KHH_SESSION_STATS));
   }
   if (rc) set_err(err, errlen, e);
@@ -245,6 +246,16 @@ int khh_session_set_test_hooks(khh_session* s, uint32_t cand_cap, int use_gate, 
   s->s.config().record_candidates = record != 0;
   s->record = record != 0;
   return s->s.set_test_hooks(cand_cap, use_gate != 0, l1_concat);
+}
+
+int khh_session_set_check_mode(khh_session* s, int mode) {
+  if (!s) return KHB_EINVAL;
+  return s->s.set_check_mode(mode);
+}
+
+void khh_gtable(uint8_t out[32 * 256 * 64]) {
+  const std::vector<uint8_t>& g = gtable_be();
+  memcpy(out, g.data(), g.size());
 }
 
 uint64_t khh_session_recorded(const khh_session* s, uint8_t* bases_be, uint32_t* targets, uint32_t* a, uint64_t cap) {

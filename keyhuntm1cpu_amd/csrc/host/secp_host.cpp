@@ -330,4 +330,27 @@ Pt pt_from_be(const uint8_t in[64]) {
   return p;
 }
 
+// Secp256K1::Init (SECP256K1.cpp:43-54): N = G; per window i: GTable[256i] = N, N = 2N, then
+// GTable[256i + j] = N, N += GTable[256i] for j < 255, GTable[256i + 255] = N.  The same chain of
+// DoubleDirect / AddDirect, so every entry is the reference's point.
+const std::vector<uint8_t>& gtable_be() {
+  static std::once_flag once;
+  static std::vector<uint8_t> tab;
+  std::call_once(once, [] {
+    tab.assign(32 * 256 * 64, 0);
+    Pt n = secp_g();
+    for (int i = 0; i < 32; ++i) {
+      const Pt w = n;
+      pt_to_be(tab.data() + 64 * (256 * i), w);
+      n = double_direct(n);
+      for (int j = 1; j < 255; ++j) {
+        pt_to_be(tab.data() + 64 * (256 * i + j), n);
+        n = add_direct(n, w);
+      }
+      pt_to_be(tab.data() + 64 * (256 * i + 255), n);
+    }
+  });
+  return tab;
+}
+
 }  // namespace khb

@@ -6,6 +6,7 @@
 #pragma once
 #include <stdint.h>
 #include <string>
+#include <vector>
 
 #include "fh.hpp"
 #include "u256.hpp"
@@ -39,6 +40,9 @@ bool on_curve(const Pt& p);
 bool parse_pubkey_hex(const char* s, Pt& out, bool& compressed, std::string* err);
 std::string pubkey_hex(const Pt& p, bool compressed);
 void pt_to_be(uint8_t out[64], const Pt& p);
+// Secp256K1::Init's GTable (SECP256K1.cpp:43-54) as 32*256 points x||y BE: entry 256*i + j = (j+1)*2^(8i)*G
+// for j < 255, entry 256*i + 255 = 2^(8(i+1))*G (the reference's "dummy" point).  Built once, cached.
+const std::vector<uint8_t>& gtable_be();
 Pt pt_from_be(const uint8_t in[64]);
 
 }  // namespace khb

@@ -8,6 +8,7 @@
 #include <new>
 #include <vector>
 #include "scan_kernels.hpp"
+#include "check_kernel.hpp"
 #include <utility>
 
 using namespace khbk;
@@ -154,6 +155,16 @@ struct khb_ctx {
   // -m address
   uint8_t* d_abloom = nullptr;
   BloomGeom ageom{};
+  // second / third check (khb_load_check_tables, khb_check): tables, a high-priority stream of its own
+  // and buffers grown to the largest batch
+  khb::CheckTables ck{};
+  void* d_ck = nullptr;                // one allocation holding every check table
+  bool ck_loaded = false;
+  hipStream_t ck_stream = nullptr;
+  CheckIn* d_ck_in = nullptr;
+  CheckOut* d_ck_out = nullptr;
+  khb::CPt* d_ck_targets = nullptr;
+  uint32_t ck_cap = 0, ck_tcap = 0;
 };
 
 namespace {
@@ -454,6 +465,14 @@ int khb_close(khb_ctx* c) {
   for (Slot& S : c->slot) free_slot(S);
   if (c->epoch) hipEventDestroy(c->epoch);
   if (c->epoch_prev) hipEventDestroy(c->epoch_prev);
+  if (c->ck_stream) {
+    hipStreamSynchronize(c->ck_stream);
+    hipStreamDestroy(c->ck_stream);
+  }
+  hipFree(c->d_ck);
+  hipFree(c->d_ck_in);
+  hipFree(c->d_ck_out);
+  hipFree(c->d_ck_targets);
   hipFree(c->d_bloom);
   hipFree(c->d_gate);
   hipFree(c->d_gate1);
@@ -833,6 +852,155 @@ int khb_hash160(khb_ctx* c, int kind, const uint8_t* xy, uint8_t* out, uint32_t 
 
 
 // ------------------------------------------------------------------------- baby-step tables
+// ------------------------------------------------------------------- second / third check (§8(f)3)
+namespace {
+
+void cpts_from_be(khb::CPt* dst, const uint8_t* src, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) {
+    fe_from_be(dst[i].x, src + 64 * (size_t)i);
+    fe_from_be(dst[i].y, src + 64 * (size_t)i + 32);
+  }
+}
+
+khb::U8 u8_from_be(const uint8_t* be) {
+  Fe f;
+  fe_from_be(f, be);
+  khb::U8 r;
+  memcpy(r.v, f.v, sizeof r.v);
+  return r;
+}
+
+BloomGeom bloom_geom(uint64_t bytes_per_sub, uint64_t bits, uint32_t hashes) {
+  BloomGeom g{};
+  g.bytes_per_sub = bytes_per_sub;
+  g.bits = bits;
+  g.magic = (uint64_t)(((unsigned __int128)1 << 64) / bits);
+  g.wrap = (uint64_t)(((unsigned __int128)1 << 64) % bits);
+  g.hashes = hashes;
+  return g;
+}
+
+bool bloom_args_ok(const uint8_t* bf, uint64_t bytes, uint64_t bits, uint32_t hashes) {
+  return bf && bytes && bits >= 2 && (bits + 7) / 8 == bytes && hashes && hashes <= 255;   // bloom.cpp:110-113
+}
+
+int ensure_check_buffers(khb_ctx* c, uint32_t n, uint32_t n_targets) {
+  if (n > c->ck_cap) {
+    hipFree(c->d_ck_in);
+    hipFree(c->d_ck_out);
+    c->d_ck_in = nullptr;
+    c->d_ck_out = nullptr;
+    c->ck_cap = 0;
+    const uint32_t cap = n < 4096 ? 4096 : n;
+    KHB_TRY(c, hipMalloc(&c->d_ck_in, sizeof(CheckIn) * cap));
+    KHB_TRY(c, hipMalloc(&c->d_ck_out, sizeof(CheckOut) * cap));
+    c->ck_cap = cap;
+  }
+  if (n_targets > c->ck_tcap) {
+    hipFree(c->d_ck_targets);
+    c->d_ck_targets = nullptr;
+    c->ck_tcap = 0;
+    const uint32_t cap = n_targets < 256 ? 256 : n_targets;
+    KHB_TRY(c, hipMalloc(&c->d_ck_targets, sizeof(khb::CPt) * cap));
+    c->ck_tcap = cap;
+  }
+  return KHB_OK;
+}
+
+}  // namespace
+
+int khb_load_check_tables(khb_ctx* c, const khb_check_tables* t) {
+  if (!c || !t || !t->gtable || !t->amp2 || !t->amp3 || !t->bptable || t->m3 == 0 || t->m3 > (1ull << 40))
+    return KHB_EINVAL;
+  if (!bloom_args_ok(t->l2, t->l2_bytes_per_sub, t->l2_bits_per_sub, t->l2_hashes) ||
+      !bloom_args_ok(t->l3, t->l3_bytes_per_sub, t->l3_bits_per_sub, t->l3_hashes))
+    return KHB_EINVAL;
+  KHB_TRY(c, hipSetDevice(c->device));
+  auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+  const size_t n_g = 32 * 256, o_g = 0, o_a2 = up(o_g + sizeof(khb::CPt) * n_g), o_a3 = up(o_a2 + sizeof(khb::CPt) * 32);
+  const size_t b2 = 256 * (size_t)t->l2_bytes_per_sub, b3 = 256 * (size_t)t->l3_bytes_per_sub;
+  const size_t o_l2 = up(o_a3 + sizeof(khb::CPt) * 32), o_l3 = up(o_l2 + b2), o_bp = up(o_l3 + b3);
+  const size_t total = o_bp + 16 * (size_t)t->m3;
+  std::vector<uint8_t> h;
+  try {
+    h.assign(total, 0);
+  } catch (const std::bad_alloc&) {
+    return KHB_ENOMEM;
+  }
+  cpts_from_be((khb::CPt*)(h.data() + o_g), t->gtable, (uint32_t)n_g);
+  cpts_from_be((khb::CPt*)(h.data() + o_a2), t->amp2, 32);
+  cpts_from_be((khb::CPt*)(h.data() + o_a3), t->amp3, 32);
+  memcpy(h.data() + o_l2, t->l2, b2);
+  memcpy(h.data() + o_l3, t->l3, b3);
+  memcpy(h.data() + o_bp, t->bptable, 16 * (size_t)t->m3);
+  if (c->ck_stream) KHB_TRY(c, hipStreamSynchronize(c->ck_stream));
+  hipFree(c->d_ck);
+  c->d_ck = nullptr;
+  c->ck_loaded = false;
+  KHB_TRY(c, hipMalloc(&c->d_ck, total));
+  KHB_TRY(c, hipMemcpy(c->d_ck, h.data(), total, hipMemcpyHostToDevice));
+  uint8_t* d = (uint8_t*)c->d_ck;
+  khb::CheckTables& T = c->ck;
+  T.gtab = (const khb::CPt*)(d + o_g);
+  T.amp2 = (const khb::CPt*)(d + o_a2);
+  T.amp3 = (const khb::CPt*)(d + o_a3);
+  T.l2 = d + o_l2;
+  T.l3 = d + o_l3;
+  T.bp = d + o_bp;
+  T.g2 = bloom_geom(t->l2_bytes_per_sub, t->l2_bits_per_sub, t->l2_hashes);
+  T.g3 = bloom_geom(t->l3_bytes_per_sub, t->l3_bits_per_sub, t->l3_hashes);
+  T.n_bp = t->m3;
+  T.m_double = u8_from_be(t->m_double_be);
+  T.m2_double = u8_from_be(t->m2_double_be);
+  T.m3 = u8_from_be(t->m3_be);
+  T.m3_double = u8_from_be(t->m3_double_be);
+  c->ck_loaded = true;
+  return KHB_OK;
+}
+
+int khb_check(khb_ctx* c, const uint8_t* targets_xy, uint32_t n_targets, const khb_check_in* in, uint32_t n,
+              khb_check_out* out) {
+  if (!c || (n && (!in || !out)) || (n_targets && !targets_xy)) return KHB_EINVAL;
+  if (!c->ck_loaded) return KHB_ESTATE;
+  if (n == 0) return KHB_OK;
+  for (uint32_t i = 0; i < n; ++i)
+    if (in[i].target >= n_targets) return KHB_EINVAL;
+  KHB_TRY(c, hipSetDevice(c->device));
+  if (!c->ck_stream) {
+    int lo = 0, hi = 0;
+    KHB_TRY(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    KHB_TRY(c, hipStreamCreateWithPriority(&c->ck_stream, hipStreamNonBlocking, hi));
+  }
+  int rc = ensure_check_buffers(c, n, n_targets);
+  if (rc) return rc;
+  std::vector<CheckIn> hin(n);
+  std::vector<CheckOut> hout(n);
+  std::vector<khb::CPt> ht(n_targets);
+  for (uint32_t i = 0; i < n; ++i) {
+    hin[i].start = u8_from_be(in[i].start_be);
+    hin[i].a = in[i].a;
+    hin[i].target = in[i].target;
+  }
+  cpts_from_be(ht.data(), targets_xy, n_targets);
+  KHB_TRY(c, hipMemcpyAsync(c->d_ck_in, hin.data(), sizeof(CheckIn) * n, hipMemcpyHostToDevice, c->ck_stream));
+  KHB_TRY(c, hipMemcpyAsync(c->d_ck_targets, ht.data(), sizeof(khb::CPt) * n_targets, hipMemcpyHostToDevice,
+                            c->ck_stream));
+  launch_check(c->ck_stream, c->ck, c->d_ck_in, c->d_ck_targets, n_targets, c->d_ck_out, n);
+  KHB_TRY(c, hipGetLastError());
+  KHB_TRY(c, hipMemcpyAsync(hout.data(), c->d_ck_out, sizeof(CheckOut) * n, hipMemcpyDeviceToHost, c->ck_stream));
+  KHB_TRY(c, hipStreamSynchronize(c->ck_stream));
+  for (uint32_t i = 0; i < n; ++i) {
+    Fe k;
+    memcpy(k.v, hout[i].key.v, sizeof k.v);
+    fe_to_be(out[i].key_be, k);
+    out[i].found = hout[i].found;
+    out[i].l2_hits = hout[i].l2_hits;
+    out[i].l3_hits = hout[i].l3_hits;
+    out[i].bp_hits = hout[i].bp_hits;
+  }
+  return KHB_OK;
+}
+
 int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t groups_per_job, uint64_t l1ext,
                    uint64_t m2, uint64_t m3, const uint64_t bytes_per_sub[3], const uint64_t bits_per_sub[3],
                    const uint32_t hashes[3], uint8_t* l1, uint8_t* l2, uint8_t* l3, uint8_t* bp, uint8_t* gate,

@@ -31,6 +31,26 @@ class AddrHit(C.Structure):
     _fields_ = [("job", C.c_uint32), ("group", C.c_uint32), ("t", C.c_uint32), ("kind", C.c_uint32)]
 
 
+class CheckTables(C.Structure):     # khb_check_tables
+    _fields_ = [("gtable", C.c_char_p), ("amp2", C.c_char_p), ("amp3", C.c_char_p),
+                ("l2", C.c_char_p), ("l2_bytes_per_sub", C.c_uint64), ("l2_bits_per_sub", C.c_uint64),
+                ("l2_hashes", C.c_uint32),
+                ("l3", C.c_char_p), ("l3_bytes_per_sub", C.c_uint64), ("l3_bits_per_sub", C.c_uint64),
+                ("l3_hashes", C.c_uint32),
+                ("bptable", C.c_char_p), ("m3", C.c_uint64),
+                ("m_double_be", C.c_uint8 * 32), ("m2_double_be", C.c_uint8 * 32), ("m3_be", C.c_uint8 * 32),
+                ("m3_double_be", C.c_uint8 * 32)]
+
+
+class CheckIn(C.Structure):        # khb_check_in
+    _fields_ = [("start_be", C.c_uint8 * 32), ("a", C.c_uint32), ("target", C.c_uint32)]
+
+
+class CheckOut(C.Structure):       # khb_check_out
+    _fields_ = [("key_be", C.c_uint8 * 32), ("found", C.c_uint32), ("l2_hits", C.c_uint32),
+                ("l3_hits", C.c_uint32), ("bp_hits", C.c_uint32)]
+
+
 class Stats(C.Structure):
     _fields_ = [("n_cand", C.c_uint32), ("n_degenerate", C.c_uint32), ("giant_steps", C.c_uint64),
                 ("kernel_ms", C.c_float), ("launch_begin_ms", C.c_double), ("launch_end_ms", C.c_double),
@@ -38,7 +58,7 @@ class Stats(C.Structure):
 
 
 _libs: dict[str, C.CDLL] = {}
-KHB_ABI_VERSION = 4
+KHB_ABI_VERSION = 5
 
 
 def lib(path: str | None = None) -> C.CDLL:
@@ -98,6 +118,9 @@ def lib(path: str | None = None) -> C.CDLL:
                                     P(AddrHit), C.c_uint32, P(Stats)]
         L.khb_addr_dump.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_char_p]
         L.khb_hash160.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_char_p, C.c_uint32]
+        if hasattr(L, "khb_check"):              # ABI 5
+            L.khb_load_check_tables.argtypes = [C.c_void_p, P(CheckTables)]
+            L.khb_check.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, P(CheckIn), C.c_uint32, P(CheckOut)]
         _libs[path] = L
     return _libs[path]
 
@@ -246,3 +269,34 @@ class Engine:
         _check(self.L.khb_hash160(self.h, kind, xy, out, n), self.h, self.L)
         r = out.raw
         return [(r[21 * i:21 * i + 20], r[21 * i + 20]) for i in range(n)]
+
+    # ---- second / third check (khb_load_check_tables, khb_check) ----
+    def load_check_tables(self, gtable: bytes, amp2: bytes, amp3: bytes, l2: tuple, l3: tuple, bptable: bytes,
+                          m3: int, m_double: int, m2_double: int, m3_value: int, m3_double: int) -> None:
+        """l2 / l3: (256 sub-blooms concatenated, bytes per sub-bloom, bits, hashes) as bloom_concat gives them."""
+        assert len(gtable) == 32 * 256 * 64 and len(amp2) == len(amp3) == 32 * 64 and len(bptable) == 16 * m3
+        t = CheckTables()
+        t.gtable, t.amp2, t.amp3 = gtable, amp2, amp3
+        t.l2, t.l2_bytes_per_sub, t.l2_bits_per_sub, t.l2_hashes = l2
+        t.l3, t.l3_bytes_per_sub, t.l3_bits_per_sub, t.l3_hashes = l3
+        t.bptable, t.m3 = bptable, m3
+        for name, v in (("m_double_be", m_double), ("m2_double_be", m2_double), ("m3_be", m3_value),
+                        ("m3_double_be", m3_double)):
+            getattr(t, name)[:] = list(v.to_bytes(32, "big"))
+        self._check_keep = (gtable, amp2, amp3, l2, l3, bptable)
+        _check(self.L.khb_load_check_tables(self.h, C.byref(t)), self.h, self.L)
+
+    def check(self, targets_xy: list[bytes], cands: list[tuple[int, int, int]]) -> list[dict]:
+        """bsgs_secondcheck on the device for [(chunk base, giant step a, target index)]: per candidate
+        {"found", "key" (int or None), "l2_hits", "l3_hits", "bp_hits"}."""
+        n = len(cands)
+        ins = (CheckIn * max(1, n))()
+        for i, (base, a, k) in enumerate(cands):
+            ins[i].start_be[:] = list(base.to_bytes(32, "big"))
+            ins[i].a = a
+            ins[i].target = k
+        outs = (CheckOut * max(1, n))()
+        _check(self.L.khb_check(self.h, b"".join(targets_xy), len(targets_xy), ins, n, outs), self.h, self.L)
+        return [{"found": int(o.found), "key": int.from_bytes(bytes(o.key_be), "big") if o.found else None,
+                 "l2_hits": int(o.l2_hits), "l3_hits": int(o.l3_hits), "bp_hits": int(o.bp_hits)}
+                for o in outs[:n]]

@@ -12,8 +12,8 @@ LIB_PATH = os.path.join(LIB_DIR, "libkhhost.so")
 _lib = None
 
 
-KHH_ABI_VERSION = 4                 # include/khhost.h
-KHH_SESSION_STATS, KHH_ADDR_STATS = 9, 8
+KHH_ABI_VERSION = 5                 # include/khhost.h
+KHH_SESSION_STATS, KHH_ADDR_STATS = 11, 8
 
 
 class KhhError(RuntimeError):
@@ -69,6 +69,8 @@ def lib() -> C.CDLL:
                                          C.c_size_t]
         L.khh_session_close.argtypes = [C.c_void_p]
         L.khh_session_set_test_hooks.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_char_p]
+        L.khh_session_set_check_mode.argtypes = [C.c_void_p, C.c_int]
+        L.khh_gtable.argtypes = [C.c_char_p]
         L.khh_session_recorded.restype = C.c_uint64
         L.khh_session_recorded.argtypes = [C.c_void_p, C.c_char_p, P(C.c_uint32), P(C.c_uint32), C.c_uint64]
         L.khh_pubkey.argtypes = [C.c_char_p, C.c_char_p]
@@ -205,6 +207,20 @@ class Tables:
         raw = C.string_at(p, 16 * n.value)
         return [(raw[16 * i:16 * i + 6], int.from_bytes(raw[16 * i + 8:16 * i + 16], "little")) for i in range(n.value)]
 
+    def bptable_raw(self) -> bytes:
+        """bPtable as m3 x 16-byte struct bsgs_xvalue records (khb_check_tables.bptable)."""
+        n = C.c_uint64()
+        p = lib().khh_bptable(self.h, C.byref(n))
+        return C.string_at(p, 16 * n.value)
+
+    def check_tables(self) -> dict:
+        """Everything khb_load_check_tables takes, from these tables (Engine.load_check_tables(**...))."""
+        l2, nb2, bits2, h2 = self.bloom_concat(2)
+        l3, nb3, bits3, h3 = self.bloom_concat(3)
+        return {"gtable": gtable(), "amp2": self.amp_table(2), "amp3": self.amp_table(3),
+                "l2": (l2, nb2, bits2, h2), "l3": (l3, nb3, bits3, h3), "bptable": self.bptable_raw(), "m3": self.m3,
+                "m_double": 2 * self.m, "m2_double": 2 * self.m2, "m3_value": self.m3, "m3_double": 2 * self.m3}
+
     def chunk_centre(self, base: int, target_xy: bytes) -> bytes:
         out = C.create_string_buffer(64)
         lib().khh_chunk_centre(self.h, _b32(base), target_xy, out)
@@ -241,7 +257,15 @@ class Tables:
 
 
 _STAT_KEYS = ("chunks", "giant_steps", "candidates", "degenerate", "kernel_s", "launches", "rescans", "busy_s",
-              "shader_mhz")
+              "shader_mhz", "device_checked", "device_check_s")
+CHECK_HOST, CHECK_DEVICE, CHECK_AUTO = 0, 1, 2      # include/khhost.h KHH_CHECK_*
+
+
+def gtable() -> bytes:
+    """Secp256K1::Init's GTable as 32*256 points x||y BE (khh_gtable; khb_check_tables.gtable)."""
+    b = C.create_string_buffer(32 * 256 * 64)
+    lib().khh_gtable(b)
+    return b.raw
 
 
 class Session:
@@ -282,7 +306,14 @@ class Session:
         st["kernel_s"] = stats[4] / 1e6
         st["busy_s"] = stats[7] / 1e6
         st["shader_mhz"] = stats[8] / 1e3
+        st["device_check_s"] = stats[10] / 1e6
         return res, st
+
+    def set_check_mode(self, mode: int) -> None:
+        """Where later runs confirm candidates: CHECK_HOST (CPU pool), CHECK_DEVICE (khb_check), CHECK_AUTO."""
+        rc = lib().khh_session_set_check_mode(self.h, mode)
+        if rc:
+            raise KhhError(f"set_check_mode failed ({rc})")
 
     def set_test_hooks(self, cand_cap: int = 0, use_gate: bool = True, record: bool = False,
                        l1_concat: bytes | None = None) -> None:

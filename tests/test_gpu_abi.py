@@ -55,10 +55,10 @@ def test_session_run_writes_six(sess):
     assert b[0] == 4                                     # chunks
 
 
-@pytest.mark.parametrize("n", [0, 3, 7, 9, 12])
+@pytest.mark.parametrize("n", [0, 3, 7, 9, 11, 14])
 def test_session_run_ex_honours_stats_len(sess, n):
     b = _run(sess, "khh_session_run_ex", n)
-    assert all(b[i] == CANARY for i in range(min(n, 9), 16))
+    assert all(b[i] == CANARY for i in range(min(n, khhost.KHH_SESSION_STATS), 16))
     if n:
         assert b[0] == 4
 

@@ -134,3 +134,14 @@ def test_batched_job_centres(ora):
     target0 = ora.parse_pubkey("04" + tg[0].hex())[0]
     for c in range(60, 70):
         assert out[64 * 3 * c:64 * 3 * c + 64] == o.chunk_start(runs[0][c], target0).be64()
+
+
+def test_gtable_matches_oracle(ora):
+    """khh_gtable (khb_check_tables.gtable) is Secp256K1::Init's GTable: entry 256*i + j = (j+1) * 2^(8i) * G."""
+    from keyhuntm1cpu_amd import khhost
+    g = khhost.gtable()
+    assert len(g) == 32 * 256 * 64
+    for i in (0, 1, 7, 16, 31):
+        for j in (0, 1, 2, 127, 253, 254, 255):
+            k = ((j + 1) << (8 * i)) % ora.ORDER            # entry (31, 255) is 2^256 G
+            assert g[64 * (256 * i + j):64 * (256 * i + j + 1)] == ora.pubkey(k).be64(), (i, j)

@@ -36,3 +36,10 @@ def test_device_math_headers_on_host(tmp_path):
 def test_hash160_header_on_host(tmp_path):
     out = _build_and_run("test_hash160_host.cpp", tmp_path)
     assert "ok" in out
+
+
+def test_confirm_header_on_host(tmp_path):
+    """device/confirm.hpp (khb_check's second/third check) vs the oracle's bsgs_secondcheck: planted keys,
+    the AddDirect(P, -P) special case, random candidates, and every level-2/3 bloom bit set."""
+    out = _build_and_run("test_confirm_host.cpp", tmp_path)
+    assert out.strip().endswith("ok"), out

@@ -8,7 +8,7 @@ OBJ=build/variants/$NAME
 mkdir -p $OUT $OBJ
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value $*"
 pids=()
-for s in khbsgs k_bsgs k_addr k_baby; do
+for s in khbsgs k_bsgs k_addr k_baby k_check; do
   /opt/rocm/bin/hipcc $FLAGS -c -o $OBJ/$s.o keyhuntm1cpu_amd/csrc/$s.hip & pids+=($!)
 done
 for p in ${pids[@]}; do wait $p; done
