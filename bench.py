@@ -172,6 +172,12 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=60.0,
                     help="CPU-baseline window (BASELINE.md: 60 s steady state after the table build)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gate", action="store_true",
+                    help="no level-0 gate: every giant step probes the level-1 bloom (the reference's exact candidate "
+                         "stream, ~1e-6 false positives per step); not the headline configuration")
+    ap.add_argument("--check", choices=("host", "gpu", "auto"), default="host",
+                    help="where candidates are confirmed (bsgs_secondcheck): the host pool (default), the GPU "
+                         "(khb_check) or auto (the GPU for batches of more than 4096 candidates)")
     # launcher self-test (tests/test_launch.py): every rank joins the gloo world and rank 0 prints the
     # ranks' view; no GPU is touched.  --launch-check-fail R makes rank R exit with status 3.
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
@@ -265,6 +271,9 @@ def main():
                 % (line[:16], world))
         cpu_base = lo
     sess = khhost.Session(tables, devices=[local], chunks_per_batch=args.chunks, check_threads=host_threads)
+    if args.no_gate:
+        sess.set_test_hooks(use_gate=False)
+    sess.set_check_mode({"host": khhost.CHECK_HOST, "gpu": khhost.CHECK_DEVICE, "auto": khhost.CHECK_AUTO}[args.check])
 
     def sync():
         torch.cuda.synchronize()
@@ -419,7 +428,9 @@ def main():
                                 "external (WORLD_SIZE set)") if world > 1 else "none",
                    "batch_note": chunks_note,
                    "ref_keys_per_s": "%.3e" % (gsps * 2 * tables.m),
-                   "candidates": st["candidates"], "found": [hex(r) if r else None for r in res]},
+                   "candidates": st["candidates"], "found": [hex(r) if r else None for r in res],
+                   "level0_gate": not args.no_gate, "check": args.check,
+                   "device_checked": st["device_checked"], "device_check_s": round(st["device_check_s"], 4)},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
