@@ -43,6 +43,7 @@ void menu() {
   printf("-p port     TCP port Number for listening conections\n");
   printf("-g ids      GPU ordinals (default 0)\n");
   printf("--cpu-build build the baby-step tables on the CPU\n");
+  printf("--check w   confirm candidates on the host, the gpu, or auto (default host)\n");
   exit(EXIT_FAILURE);
 }
 
@@ -126,7 +127,9 @@ int main(int argc, char** argv) {
   std::string ip = "127.0.0.1";
   SearchConfig cfg;
   if (nthreads > 16) nthreads = 16;
-  static struct option longopts[] = {{"cpu-build", no_argument, nullptr, 1000}, {nullptr, 0, nullptr, 0}};
+  static struct option longopts[] = {{"cpu-build", no_argument, nullptr, 1000},
+                                     {"check", required_argument, nullptr, 1001},
+                                     {nullptr, 0, nullptr, 0}};
   int c;
   while ((c = getopt_long(argc, argv, "6hk:n:t:p:i:g:", longopts, nullptr)) != -1) {
     switch (c) {
@@ -164,6 +167,12 @@ int main(int argc, char** argv) {
         break;
       }
       case 1000: cpu_build = true; break;
+      case 1001:                                    // where candidates are confirmed (engine.hpp check_mode)
+        if (!strcmp(optarg, "host")) cfg.check_mode = kCheckHost;
+        else if (!strcmp(optarg, "gpu")) cfg.check_mode = kCheckDevice;
+        else if (!strcmp(optarg, "auto")) cfg.check_mode = kCheckAuto;
+        else { fprintf(stderr, "[E] --check: host, gpu or auto\n"); exit(EXIT_FAILURE); }
+        break;
       default:
         fprintf(stderr, "[E] Unknow opcion -%c\n", c);
         exit(0);

@@ -36,13 +36,14 @@ def _ask(port: int, line: bytes) -> str:
     return data.decode()
 
 
-@pytest.fixture(scope="module")
-def daemon(tmp_path_factory):
+@pytest.fixture(scope="module", params=["host", "gpu"])
+def daemon(tmp_path_factory, request):
+    """The daemon with its candidates confirmed on the host pool, then on the GPU (--check gpu, khb_check)."""
     cwd = tmp_path_factory.mktemp("bsgsd")
     port = _free_port()
     log = open(cwd / "bsgsd.log", "w")
-    p = subprocess.Popen([os.path.join(BIN_DIR, "bsgsd_amd"), "-k", "1", "-t", "8", "-p", str(port)], cwd=cwd,
-                         stdout=log, stderr=subprocess.STDOUT)
+    p = subprocess.Popen([os.path.join(BIN_DIR, "bsgsd_amd"), "-k", "1", "-t", "8", "-p", str(port), "--check",
+                          request.param], cwd=cwd, stdout=log, stderr=subprocess.STDOUT)
     t0 = time.time()
     while time.time() - t0 < 180:
         if p.poll() is not None:

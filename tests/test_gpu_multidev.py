@@ -41,6 +41,16 @@ def test_cli_two_contexts_puzzle63(tmp_path):
     assert (tmp_path / "KEYFOUNDKEYFOUND.txt").read_text().count("Key found privkey") == 1
 
 
+def test_cli_two_contexts_device_check(tmp_path):
+    """-g 0,0 --check gpu: each device thread confirms its own batches on its own context (khb_check)."""
+    (tmp_path / "63.pub").write_text(P63 + "\n")
+    r = _cli(["-m", "bsgs", "-f", "63.pub", "-r", "7cce500000000000:7cce600000000000", "-n", "0x1000000000",
+              "-g", "0,0", "--gpu-blocks", str(LANES // 256), "--check", "gpu", "-q", "-s", "0"], tmp_path)
+    assert r.returncode == 1, r.stdout + r.stderr
+    assert r.stdout.count("Key found privkey") == 1
+    assert "[+] Thread Key found privkey 7cce5efdaccf6808" in r.stdout
+
+
 def test_session_two_contexts_two_targets():
     """Two targets in different chunks of one range, two contexts: each key reported once."""
     t = khhost.Tables("0x1000000000", 1, threads=16)     # N = 2^36: 2^37 keys per chunk
