@@ -6,6 +6,9 @@ container, where the reference checkout is mounted read-only at /root/reference)
   puzzle_keys.json     keys of puzzles 1..45 found by the oracle BSGS search; each is
                        self-certifying: pubkey(key) equals the reference file's line
   scan_vectors.json    oracle candidate sets + x-dump digests for fixed (geometry, base, target)
+  check_vectors.json   oracle bsgs_secondcheck results (keyhunt.cpp:4271-4368) for fixed candidates:
+                       planted keys, the third check's AddDirect(P, -P) case, random candidates
+                       (`python tests/golden/make_golden.py check` rewrites only this file)
 """
 import hashlib
 import json
@@ -79,5 +82,45 @@ def main():
         json.dump(vec, f, indent=1)
 
 
+def splitmix(seed):
+    s = seed
+    while True:
+        s = (s + 0x9E3779B97F4A7C15) & (2**64 - 1)
+        z = s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & (2**64 - 1)
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & (2**64 - 1)
+        yield z ^ (z >> 31)
+
+
+def check_vectors():
+    n = "0x1000000000"
+    bs = ora.Bsgs(n, 1)
+    m, m2, m3 = bs.m, bs.m2, bs.m3
+    r = splitmix(0x676f6c64656e)
+    cases = []
+    for _ in range(12):
+        base = next(r) | ((next(r) & 0xFFFF) << 64)
+        a = next(r) % 4096
+        cases.append(("planted", base, a, base + a * 2 * m + next(r) % (2 * m + 64)))
+    for _ in range(6):
+        base, a, i2, i = next(r), next(r) % 4096, next(r) % 32, next(r) % 32
+        cases.append(("special", base, a, base + a * 2 * m + i2 * 2 * m2 + i * 2 * m3 + m3))
+    for _ in range(6):
+        cases.append(("random", next(r) | (next(r) << 64), next(r) & 0xFFFFFFFF,
+                      next(r) | (next(r) << 64) | (next(r) << 128)))
+    vec = []
+    for kind, base, a, key in cases:
+        t = ora.pubkey(key)
+        found = bs.secondcheck(base, a, t)
+        vec.append({"kind": kind, "base": hex(base), "a": a, "target": t.be64().hex(),
+                    "found": hex(found) if found is not None else None})
+    with open(os.path.join(OUT, "check_vectors.json"), "w") as f:
+        json.dump({"n": n, "k": 1, "cases": vec}, f, indent=1)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["check"]:
+        check_vectors()
+    else:
+        main()
+        check_vectors()

@@ -66,3 +66,42 @@ def test_gpu_scan_matches_golden(eng, v):
     assert st.giant_steps == v["groups"] * 1024
     assert sorted(a for _, a in cands) == sorted(v["candidates"])
     assert all(job == 0 for job, _ in cands)
+
+
+# ---- second / third check vectors (tests/golden/check_vectors.json, make_golden.py check_vectors) ----
+with open(os.path.join(HERE, "golden", "check_vectors.json")) as f:
+    CHECK = json.load(f)
+CHECK_IDS = [f"{i}-{c['kind']}" for i, c in enumerate(CHECK["cases"])]
+
+
+@pytest.fixture(scope="module")
+def check_tables():
+    from keyhuntm1cpu_amd import khhost
+    t = khhost.Tables(CHECK["n"], 1, threads=8, gpl=4)
+    yield t
+    t.close()
+
+
+def test_check_vectors_cover_every_path():
+    kinds = [c["kind"] for c in CHECK["cases"] if c["found"]]
+    assert kinds.count("planted") >= 8 and kinds.count("special") >= 4
+    assert all(c["found"] is None for c in CHECK["cases"] if c["kind"] == "random")
+
+
+@pytest.mark.parametrize("c", CHECK["cases"], ids=CHECK_IDS)
+def test_host_secondcheck_matches_golden(check_tables, c):
+    """The host engine's bsgs_secondcheck (Tables::secondcheck, the CPU pool's check) vs the fixture."""
+    got = check_tables.secondcheck(int(c["base"], 16), c["a"], bytes.fromhex(c["target"]))
+    assert (hex(got) if got is not None else None) == c["found"]
+
+
+@pytest.mark.gpu
+def test_gpu_check_matches_golden(check_tables):
+    """khb_check with the product's tables (libkhhost) vs the fixture, every case in one launch."""
+    from keyhuntm1cpu_amd.khbsgs import Engine
+    cases = CHECK["cases"]
+    with Engine(0, lanes=16384) as e:
+        e.load_check_tables(**check_tables.check_tables())
+        got = e.check([bytes.fromhex(c["target"]) for c in cases],
+                      [(int(c["base"], 16), c["a"], i) for i, c in enumerate(cases)])
+    assert [hex(g["key"]) if g["found"] else None for g in got] == [c["found"] for c in cases]

@@ -47,3 +47,16 @@ def test_puzzle63_known_answer(ora):
     t, _ = ora.parse_pubkey("0365ec2994b8cc0a20d40dd69edfe55ca32a54bcbbaa6b0ddcff36049301a54579")
     _, keys = bs.search([t], 0x7CCE500000000000, 0x7CCE600000000000)
     assert keys == [0x7CCE5EFDACCF6808]
+
+
+def test_check_vectors_reproduce_from_oracle(ora):
+    """tests/golden/check_vectors.json is the oracle's bsgs_secondcheck output (make_golden.py check_vectors)."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "check_vectors.json")) as f:
+        d = json.load(f)
+    bs = ora.Bsgs(d["n"], d["k"])
+    for c in d["cases"]:
+        t = ora.parse_pubkey("04" + c["target"])[0]
+        got = bs.secondcheck(int(c["base"], 16), c["a"], t)
+        assert (hex(got) if got is not None else None) == c["found"], c
