@@ -168,10 +168,10 @@ int main(int argc, char** argv) {
       }
       case 1000: cpu_build = true; break;
       case 1001:                                    // where candidates are confirmed (engine.hpp check_mode)
-        if (!strcmp(optarg, "host")) cfg.check_mode = kCheckHost;
-        else if (!strcmp(optarg, "gpu")) cfg.check_mode = kCheckDevice;
-        else if (!strcmp(optarg, "auto")) cfg.check_mode = kCheckAuto;
-        else { fprintf(stderr, "[E] --check: host, gpu or auto\n"); exit(EXIT_FAILURE); }
+        if ((cfg.check_mode = parse_check_mode(optarg)) < 0) {
+          fprintf(stderr, "[E] --check: host, gpu or auto\n");
+          exit(EXIT_FAILURE);
+        }
         break;
       default:
         fprintf(stderr, "[E] Unknow opcion -%c\n", c);

@@ -419,6 +419,13 @@ void device_thread(Shared& S, khb_ctx* ctx) {
 
 }  // namespace
 
+int parse_check_mode(const char* s) {
+  if (!strcmp(s, "host")) return kCheckHost;
+  if (!strcmp(s, "gpu")) return kCheckDevice;
+  if (!strcmp(s, "auto")) return kCheckAuto;
+  return -1;
+}
+
 int load_check_tables(khb_ctx* c, const Tables& T) {
   const std::vector<uint8_t> l2 = T.bloom_concat(2), l3 = T.bloom_concat(3);
   const std::vector<uint8_t> a2 = T.amp_table_be(2), a3 = T.amp_table_be(3);

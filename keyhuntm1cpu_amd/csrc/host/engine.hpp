@@ -48,6 +48,8 @@ struct SearchConfig {
 };
 enum : int { kCheckHost = 0, kCheckDevice = 1, kCheckAuto = 2 };
 constexpr uint32_t kCheckAutoMin = 4096;
+// The --check argument of keyhunt_amd / bsgsd_amd: "host", "gpu" or "auto"; -1 for anything else.
+int parse_check_mode(const char* s);
 
 struct SearchStats {
   uint64_t launches = 0;           // GPU scan launches (one per batch per device)

@@ -264,10 +264,10 @@ int main(int argc, char** argv) {
       case 1003: cfg.max_chunks = strtoull(optarg, nullptr, 10); break;
       case 1004: cpu_build = true; break;
       case 1005:                                    // where candidates are confirmed (engine.hpp check_mode)
-        if (!strcmp(optarg, "host")) cfg.check_mode = kCheckHost;
-        else if (!strcmp(optarg, "gpu")) cfg.check_mode = kCheckDevice;
-        else if (!strcmp(optarg, "auto")) cfg.check_mode = kCheckAuto;
-        else { fprintf(stderr, "[E] --check: host, gpu or auto\n"); exit(EXIT_FAILURE); }
+        if ((cfg.check_mode = parse_check_mode(optarg)) < 0) {
+          fprintf(stderr, "[E] --check: host, gpu or auto\n");
+          exit(EXIT_FAILURE);
+        }
         break;
       case 1006: cfg.use_gate = false; break;       // the reference's exact level-1 candidate stream
       case 'C': case 'E': case 'N': case 'p': case 'v': case 'G': case '8': case 'z':

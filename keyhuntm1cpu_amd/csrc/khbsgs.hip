@@ -185,6 +185,17 @@ void pts_from_be(AffPt* dst, const uint8_t* src, uint32_t n) {
   }
 }
 
+// A bloom level's geometry with the Barrett constants of mod_bits (bloom_probe.hpp).
+BloomGeom bloom_geom(uint64_t bytes_per_sub, uint64_t bits, uint32_t hashes) {
+  BloomGeom g{};
+  g.bytes_per_sub = bytes_per_sub;
+  g.bits = bits;
+  g.magic = (uint64_t)(((unsigned __int128)1 << 64) / bits);
+  g.wrap = (uint64_t)(((unsigned __int128)1 << 64) % bits);
+  g.hashes = hashes;
+  return g;
+}
+
 // Groups the slot's last launch walked (count_walked, copied back with the counters).
 uint64_t walked_groups(const Slot& S) {
   uint64_t v;
@@ -527,11 +538,7 @@ int khb_load_bloom(khb_ctx* c, const uint8_t* bf, uint64_t bytes_per_sub, uint64
   const size_t total = (size_t)bytes_per_sub * 256;
   KHB_TRY(c, hipMalloc(&c->d_bloom, total));
   KHB_TRY(c, hipMemcpy(c->d_bloom, bf, total, hipMemcpyHostToDevice));
-  c->geom.bytes_per_sub = bytes_per_sub;
-  c->geom.bits = bits_per_sub;
-  c->geom.magic = (uint64_t)(((unsigned __int128)1 << 64) / bits_per_sub);
-  c->geom.wrap = (uint64_t)(((unsigned __int128)1 << 64) % bits_per_sub);
-  c->geom.hashes = hashes;
+  c->geom = bloom_geom(bytes_per_sub, bits_per_sub, hashes);
   return KHB_OK;
 }
 
@@ -723,11 +730,7 @@ int khb_load_addr_bloom(khb_ctx* c, const uint8_t* bf, uint64_t bytes, uint64_t 
   if (c->d_abloom) { hipFree(c->d_abloom); c->d_abloom = nullptr; }
   KHB_TRY(c, hipMalloc(&c->d_abloom, bytes));
   KHB_TRY(c, hipMemcpy(c->d_abloom, bf, bytes, hipMemcpyHostToDevice));
-  c->ageom.bytes_per_sub = bytes;
-  c->ageom.bits = bits;
-  c->ageom.magic = (uint64_t)(((unsigned __int128)1 << 64) / bits);
-  c->ageom.wrap = (uint64_t)(((unsigned __int128)1 << 64) % bits);
-  c->ageom.hashes = hashes;
+  c->ageom = bloom_geom(bytes, bits, hashes);
   return KHB_OK;
 }
 
@@ -868,16 +871,6 @@ khb::U8 u8_from_be(const uint8_t* be) {
   khb::U8 r;
   memcpy(r.v, f.v, sizeof r.v);
   return r;
-}
-
-BloomGeom bloom_geom(uint64_t bytes_per_sub, uint64_t bits, uint32_t hashes) {
-  BloomGeom g{};
-  g.bytes_per_sub = bytes_per_sub;
-  g.bits = bits;
-  g.magic = (uint64_t)(((unsigned __int128)1 << 64) / bits);
-  g.wrap = (uint64_t)(((unsigned __int128)1 << 64) % bits);
-  g.hashes = hashes;
-  return g;
 }
 
 bool bloom_args_ok(const uint8_t* bf, uint64_t bytes, uint64_t bits, uint32_t hashes) {
@@ -1045,12 +1038,7 @@ int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t
     if (e == hipSuccess) e = hipMemsetAsync(dw[l], 0, 256 * words * 4, S.stream);
     A.bw[l] = dw[l];
     A.bwords[l] = words;
-    BloomGeom& g = A.bgeom[l];
-    g.bytes_per_sub = bytes_per_sub[l];
-    g.bits = bits_per_sub[l];
-    g.magic = (uint64_t)(((unsigned __int128)1 << 64) / g.bits);
-    g.wrap = (uint64_t)(((unsigned __int128)1 << 64) % g.bits);
-    g.hashes = hashes[l];
+    A.bgeom[l] = bloom_geom(bytes_per_sub[l], bits_per_sub[l], hashes[l]);
   }
   if (e == hipSuccess && bp && m3) {
     e = hipMalloc(&dbp, 16 * m3);
