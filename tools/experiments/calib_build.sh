@@ -12,7 +12,8 @@
 #   block_patch.py: KHB_BLOCK threads per workgroup.
 #   scr_patch.py: KHB_SCR_MASK=m keeps the prefix scratch in (i & m) entries per group (no HBM stream).
 #   addrwalk_patch.py: the -m address kernels without the hashing (count-only: the x/y walk's VALU).
-# Usage: tools/experiments/calib_build.sh pad|rm|scr|pair|defer|nonop|block|addrwalk <name> [-DKEY=VAL ...]
+#   ntst_patch.py: the prefix-scratch stores non-temporal, loads plain (timing only).
+# Usage: tools/experiments/calib_build.sh pad|rm|scr|pair|defer|nonop|block|addrwalk|ntst <name> [-DKEY=VAL ...]
 set -e
 KIND=$1; NAME=$2; shift 2
 S1=keyhuntm1cpu_amd/csrc/device/fe_asm.hpp
