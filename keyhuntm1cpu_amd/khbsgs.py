@@ -273,7 +273,8 @@ class Engine:
     # ---- second / third check (khb_load_check_tables, khb_check) ----
     def load_check_tables(self, gtable: bytes, amp2: bytes, amp3: bytes, l2: tuple, l3: tuple, bptable: bytes,
                           m3: int, m_double: int, m2_double: int, m3_value: int, m3_double: int) -> None:
-        """l2 / l3: (256 sub-blooms concatenated, bytes per sub-bloom, bits, hashes) as bloom_concat gives them."""
+        """l2 / l3: (256 sub-blooms concatenated, bytes per sub-bloom, bits, hashes) as bloom_concat gives them.
+        The library copies every table to the device before it returns."""
         assert len(gtable) == 32 * 256 * 64 and len(amp2) == len(amp3) == 32 * 64 and len(bptable) == 16 * m3
         t = CheckTables()
         t.gtable, t.amp2, t.amp3 = gtable, amp2, amp3
@@ -283,7 +284,6 @@ class Engine:
         for name, v in (("m_double_be", m_double), ("m2_double_be", m2_double), ("m3_be", m3_value),
                         ("m3_double_be", m3_double)):
             getattr(t, name)[:] = list(v.to_bytes(32, "big"))
-        self._check_keep = (gtable, amp2, amp3, l2, l3, bptable)
         _check(self.L.khb_load_check_tables(self.h, C.byref(t)), self.h, self.L)
 
     def check(self, targets_xy: list[bytes], cands: list[tuple[int, int, int]]) -> list[dict]:
