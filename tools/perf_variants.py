@@ -45,16 +45,24 @@ if int(os.environ.get("GATE_ZERO", "0") or 0):
 # One Engine at a time: each owns ~26 GB of scratch per submission slot, so every (variant, gate) pair
 # gets its own context per round, opened, timed and closed before the next one (round 3 kept all of them
 # open at once and ran out of HBM with six variants, gpurun_out/r03m/ab.txt).
-configs = [(p, g) for p in paths for g in gsets]
+# STAGE1=0,22: also time every real gate with a stage-1 fold of 2^22 bytes (khb_set_gate_stage1; 0 = the
+# library default, which folds only gates larger than 32 MiB)
+stage1s = [int(v) for v in os.environ.get("STAGE1", "0").split(",") if v]
+configs = [(p, (g, s1)) for p in paths for g in gsets for s1 in (stage1s if g > 0 else [0])]
 
 
-def cfg_name(p, g):
-    return os.path.basename(p) + (f" +gate{g}" if g > 0 else f" +zerogate{-g}" if g else "")
+def cfg_name(p, gs):
+    g, s1 = gs
+    return (os.path.basename(p) + (f" +gate{g}" if g > 0 else f" +zerogate{-g}" if g else "")
+            + (f" +stage1 2^{s1}B" if s1 else ""))
 
 
-def open_engine(p, g):
+def open_engine(p, gs):
+    g, s1 = gs
     e = Engine(0, lib_path=p)
     e.load_bloom(bf, nb, bits, h)
+    if s1:
+        e.set_gate_stage1(s1)
     if g:
         e.load_gate(gates[g], abs(g), t.gate_probes())
     e.load_giant_table(gsn)
@@ -63,14 +71,15 @@ def open_engine(p, g):
     return e
 
 
-times = {cfg_name(p, g): [] for p, g in configs}
+times = {cfg_name(p, gs): [] for p, gs in configs}
 mhz = {n: [] for n in times}
 ncand = {}
 ref = {}
 for rnd in range(int(os.environ.get("ROUNDS", "3"))):
-    for p, g in configs:
-        n = cfg_name(p, g)
-        e = open_engine(p, g)
+    for p, gs in configs:
+        g = gs[0]
+        n = cfg_name(p, gs)
+        e = open_engine(p, gs)
         try:
             if rnd == 0:
                 print(f"{n}: lanes {e.lanes()}", flush=True)
@@ -94,5 +103,5 @@ for g in ref:   # a gate keeps a subset of the L1 candidates
 steps = jobs * t.cycles * 1024
 for n in times:
     med = statistics.median(times[n])
-    print(f"{n:34s} median {med:8.2f} ms  min {min(times[n]):8.2f}  {steps / med / 1e6:8.3f} G steps/s"
+    print(f"{n:48s} median {med:8.2f} ms  min {min(times[n]):8.2f}  {steps / med / 1e6:8.3f} G steps/s"
           f"  cand {ncand[n]}  clock {statistics.median(mhz[n]):7.1f} MHz", flush=True)
