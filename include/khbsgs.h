@@ -131,9 +131,11 @@ int khb_load_gate(khb_ctx* ctx, const uint8_t* gate, uint32_t log2_bits, uint32_
 /* Stage-1 fold for gates loaded after this call: a gate larger than 2^log2_bytes bytes is also kept
  * OR-folded to 2^log2_bytes bytes (block i of the fold = OR of the gate's blocks j with
  * j mod (2^log2_bytes / 8) == i).  x tests its block of the fold first and reads its block of the
- * full gate only when those bits are all set: the same candidates, fewer random reads of a gate
- * that does not fit the Infinity Cache beside the level-1 bloom (k >= 4).  0 = no stage 1;
- * otherwise log2_bytes in [10, 31].  Default 25 (32 MiB: no fold at k = 1, a 4x fold at k = 4). */
+ * full gate only when those bits are all set: the same candidates, and most tests served by a fold
+ * small enough for the L2 (k = 1) or by one that fits the Infinity Cache beside the level-1 bloom
+ * (k >= 4).  0 = no stage 1; otherwise log2_bytes in [10, 31], or KHB_GATE_STAGE1_AUTO (the default):
+ * 2 MiB for a gate of up to 32 MiB, 32 MiB for a larger one. */
+#define KHB_GATE_STAGE1_AUTO 1
 int khb_set_gate_stage1(khb_ctx* ctx, uint32_t log2_bytes);
 /* GSn[0..511] and _2GSn (keyhunt.cpp:1325-1338), 513 affine points x||y BE. */
 int khb_load_giant_table(khb_ctx* ctx, const uint8_t* gsn_xy_be);

@@ -509,9 +509,13 @@ int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t 
   KHB_TRY(c, hipMemcpy(c->d_gate, gate, bytes, hipMemcpyHostToDevice));
   c->gate_mask = (uint32_t)((1ull << (log2_bits - 6)) - 1);
   c->gate_probes = probes;
-  if (c->gate1_log2 && (size_t)1 << c->gate1_log2 < bytes) {
-    // stage 1: the gate OR-folded to 2^gate1_log2 bytes (a superset: no member is ever dropped)
-    const size_t nb1 = ((size_t)1 << c->gate1_log2) / 8, nb = bytes / 8;
+  // KHB_GATE_STAGE1_AUTO: an L2-sized 2 MiB fold of a gate of up to 32 MiB (k = 1: -6.4 % time,
+  // profiles/r04g_k1/ab.txt), a 32 MiB fold of a larger one (k = 4: 128 MiB beside the 57.5 MiB L1 bloom,
+  // where a 4 MiB fold measured 3.5 % slower and 8 / 16 MiB the same, profiles/r04g_k1/k4.txt)
+  const uint32_t f_log2 = c->gate1_log2 != KHB_GATE_STAGE1_AUTO ? c->gate1_log2 : bytes <= (1u << 25) ? 21u : 25u;
+  if (f_log2 && (size_t)1 << f_log2 < bytes) {
+    // stage 1: the gate OR-folded to 2^f_log2 bytes (a superset: no member is ever dropped)
+    const size_t nb1 = ((size_t)1 << f_log2) / 8, nb = bytes / 8;
     std::vector<uint64_t> f(nb1, 0);
     const uint64_t* g = reinterpret_cast<const uint64_t*>(gate);
     for (size_t j = 0; j < nb; ++j) f[j & (nb1 - 1)] |= g[j];
@@ -523,7 +527,8 @@ int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t 
 }
 
 int khb_set_gate_stage1(khb_ctx* c, uint32_t log2_bytes) {
-  if (!c || (log2_bytes && (log2_bytes < 10 || log2_bytes > 31))) return KHB_EINVAL;
+  if (!c || (log2_bytes && log2_bytes != KHB_GATE_STAGE1_AUTO && (log2_bytes < 10 || log2_bytes > 31)))
+    return KHB_EINVAL;
   if (c->queued) return KHB_EBUSY;
   c->gate1_log2 = log2_bytes;
   return KHB_OK;

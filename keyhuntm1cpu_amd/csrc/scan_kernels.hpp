@@ -29,7 +29,7 @@ struct AffPt {
 };
 
 #ifndef KHB_GATE1
-#define KHB_GATE1 25              // default log2 bytes of the stage-1 fold of a larger level-0 gate (0 = none)
+#define KHB_GATE1 1               // default stage-1 fold of the level-0 gate: KHB_GATE_STAGE1_AUTO (khbsgs.h)
 #endif
 #ifndef KHB_WAVES_PER_SIMD
 // occupancy target of k_giant_scan (launch bounds).  Round 3: 3 waves/SIMD (168 VGPRs, 196,608 lanes)

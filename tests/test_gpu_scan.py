@@ -244,6 +244,6 @@ def test_gate_candidates_exact(eng, bs32, ora, probes):
         assert 0.4 < sum(map(len, gate_ref)) / sum(map(len, l1_ref)) < 0.6
         assert sum(map(len, l1_ref)) > 100000
     finally:
-        eng.set_gate_stage1(25)
+        eng.set_gate_stage1(1)                 # KHB_GATE_STAGE1_AUTO, the library default
         eng.load_gate(None)
         load_tables(eng, bs32, gpl)

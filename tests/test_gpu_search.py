@@ -145,8 +145,15 @@ def test_full_geometry_gate(tables_k1, ora):
         e.load_lane_offsets(offs, gpl)
         centres = [tables_k1.chunk_centre(b, t.be64()) for b in bases]
         plain, _, _ = e.scan(b"".join(centres), 0, tables_k1.cycles)
-        e.load_gate(gate, lg, probes)
-        gated, _, st = e.scan(b"".join(centres), 0, tables_k1.cycles)
+        # the product default (KHB_GATE_STAGE1_AUTO: a 2 MiB stage-1 fold in front of the 32 MiB gate),
+        # no fold, and a 4 MiB fold give the same candidates
+        by_fold = {}
+        for stage1 in (0, 22, 1):
+            e.set_gate_stage1(stage1)
+            e.load_gate(gate, lg, probes)
+            by_fold[stage1], _, st = e.scan(b"".join(centres), 0, tables_k1.cycles)
+        gated = by_fold[1]
+        assert sorted(by_fold[0]) == sorted(by_fold[22]) == sorted(gated)
         exp = []
         for j, a in plain:
             g0 = (a // 1024) // gpl * gpl
@@ -232,12 +239,12 @@ def test_k4_full_geometry_candidates_match_oracle(tables_k4, ora):
         # the product gate at k = 4 (2^30 bits, 128 MiB) with and without its 32 MiB stage-1 fold
         gate, lg = tables_k4.gate()
         gated = {}
-        for stage1 in (0, 25):
+        for stage1 in (0, 25, 1):              # 1 = KHB_GATE_STAGE1_AUTO (32 MiB at k = 4)
             e.set_gate_stage1(stage1)
             e.load_gate(gate, lg, tables_k4.gate_probes())
             gated[stage1], gdegen, _ = e.scan(centres, 0, tables_k4.cycles)
             assert not gdegen
-    assert sorted(gated[25]) == sorted(gated[0])
+    assert sorted(gated[25]) == sorted(gated[0]) == sorted(gated[1])
     assert set(gated[0]) <= set(got)
     assert any(tables_k4.secondcheck(bases[0], a, t.be64()) == key for jj, a in gated[25] if jj == 0)
     assert not degen
