@@ -45,24 +45,24 @@ if int(os.environ.get("GATE_ZERO", "0") or 0):
 # One Engine at a time: each owns ~26 GB of scratch per submission slot, so every (variant, gate) pair
 # gets its own context per round, opened, timed and closed before the next one (round 3 kept all of them
 # open at once and ran out of HBM with six variants, gpurun_out/r03m/ab.txt).
-# STAGE1=0,22: also time every real gate with a stage-1 fold of 2^22 bytes (khb_set_gate_stage1; 0 = the
-# library default, which folds only gates larger than 32 MiB)
-stage1s = [int(v) for v in os.environ.get("STAGE1", "0").split(",") if v]
-configs = [(p, (g, s1)) for p in paths for g in gsets for s1 in (stage1s if g > 0 else [0])]
+# STAGE1=default,0,22: time every real gate with the library's default stage-1 fold (KHB_GATE_STAGE1_AUTO),
+# with none (0), and with a fold of 2^22 bytes (khb_set_gate_stage1)
+stage1s = [v for v in os.environ.get("STAGE1", "default").split(",") if v]
+configs = [(p, (g, s1)) for p in paths for g in gsets for s1 in (stage1s if g > 0 else ["default"])]
 
 
 def cfg_name(p, gs):
     g, s1 = gs
     return (os.path.basename(p) + (f" +gate{g}" if g > 0 else f" +zerogate{-g}" if g else "")
-            + (f" +stage1 2^{s1}B" if s1 else ""))
+            + ("" if s1 == "default" else " +no stage1" if s1 == "0" else f" +stage1 2^{s1}B"))
 
 
 def open_engine(p, gs):
     g, s1 = gs
     e = Engine(0, lib_path=p)
     e.load_bloom(bf, nb, bits, h)
-    if s1:
-        e.set_gate_stage1(s1)
+    if s1 != "default":
+        e.set_gate_stage1(int(s1))
     if g:
         e.load_gate(gates[g], abs(g), t.gate_probes())
     e.load_giant_table(gsn)
@@ -71,6 +71,9 @@ def open_engine(p, gs):
     return e
 
 
+# PIPE=n (n >= 2): time n back-to-back launches with two in flight, as the engine runs them, instead of one
+# synchronous launch (whose ramp and tail the queue otherwise hides)
+pipe = int(os.environ.get("PIPE", "0") or 0)
 times = {cfg_name(p, gs): [] for p, gs in configs}
 mhz = {n: [] for n in times}
 ncand = {}
@@ -83,10 +86,21 @@ for rnd in range(int(os.environ.get("ROUNDS", "3"))):
         try:
             if rnd == 0:
                 print(f"{n}: lanes {e.lanes()}", flush=True)
-            c, d, st = e.scan(centres, 0, t.cycles)
+            if pipe:
+                # PIPE=n: n launches with two in flight (the engine's queue depth), wall time per launch
+                e.submit(centres, 0, t.cycles)
+                t0 = time.perf_counter()
+                for _ in range(pipe - 1):
+                    e.submit(centres, 0, t.cycles)
+                    c, d, st = e.collect()
+                c, d, st = e.collect()
+                kms = 1e3 * (time.perf_counter() - t0) / pipe
+            else:
+                c, d, st = e.scan(centres, 0, t.cycles)
+                kms = st.kernel_ms
         finally:
             e.close()
-        times[n].append(st.kernel_ms)
+        times[n].append(kms)
         mhz[n].append(getattr(st, "shader_mhz", 0.0))
         ncand[n] = len(c)
         timing_only = [v for v in os.environ.get("TIMING_ONLY", "").split(",") if v]
