@@ -72,10 +72,21 @@ constexpr size_t kCounterBytes = 64;                 // ScanArgs::counters
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-// Prefix-scratch stream (written once by the forward pass, read once by the walk).  Non-temporal
-// accesses were measured slower (profiles/r01_gate_experiments_raw.txt), so these are plain.
-__device__ __forceinline__ void scr_st(Fe* p, const Fe& v) { *p = v; }
-__device__ __forceinline__ Fe scr_ld(const Fe* p) { return *p; }
+// Prefix-scratch stream (written once by the forward pass, read once by the walk ~512 steps later, from
+// HBM: 26 GB per slot).  Non-temporal loads and stores keep it from displacing the level-0 gate's L2-sized
+// stage-1 fold (khb_set_gate_stage1): -1.5 % time with two launches in flight, -0.3 % as one launch
+// (profiles/r04i/nt_ab.txt, r04h/ntall_ab.txt).  Without the fold (round 1, 4 waves/SIMD) they measured
+// slower (profiles/r01_gate_experiments_raw.txt); tools/experiments/plainscr_patch.py builds the plain form.
+__device__ __forceinline__ void scr_st(Fe* p, const Fe& v) {
+  v4u* q = reinterpret_cast<v4u*>(p);
+  __builtin_nontemporal_store(v4u{v.v[0], v.v[1], v.v[2], v.v[3]}, q);
+  __builtin_nontemporal_store(v4u{v.v[4], v.v[5], v.v[6], v.v[7]}, q + 1);
+}
+__device__ __forceinline__ Fe scr_ld(const Fe* p) {
+  const v4u* q = reinterpret_cast<const v4u*>(p);
+  const v4u lo = __builtin_nontemporal_load(q), hi = __builtin_nontemporal_load(q + 1);
+  return Fe{{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w}};
+}
 
 struct ScanArgs {
   const uint8_t* __restrict__ bloom;

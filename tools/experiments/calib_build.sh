@@ -12,9 +12,8 @@
 #   block_patch.py: KHB_BLOCK threads per workgroup.
 #   scr_patch.py: KHB_SCR_MASK=m keeps the prefix scratch in (i & m) entries per group (no HBM stream).
 #   addrwalk_patch.py: the -m address kernels without the hashing (count-only: the x/y walk's VALU).
-#   ntst_patch.py: the prefix-scratch stores non-temporal, loads plain (timing only).
-#   ntld_patch.py: the prefix-scratch loads non-temporal (KHB_NT_ST=1: the stores too).
-# Usage: tools/experiments/calib_build.sh pad|rm|scr|pair|defer|nonop|block|addrwalk|ntst|ntld <name> [-DKEY=VAL ...]
+#   plainscr_patch.py: the prefix-scratch stream with plain loads and stores (the product's are non-temporal).
+# Usage: tools/experiments/calib_build.sh pad|rm|scr|pair|defer|nonop|block|addrwalk|plainscr <name> [-DKEY=VAL ...]
 set -e
 KIND=$1; NAME=$2; shift 2
 S1=keyhuntm1cpu_amd/csrc/device/fe_asm.hpp
