@@ -509,10 +509,11 @@ int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t 
   KHB_TRY(c, hipMemcpy(c->d_gate, gate, bytes, hipMemcpyHostToDevice));
   c->gate_mask = (uint32_t)((1ull << (log2_bits - 6)) - 1);
   c->gate_probes = probes;
-  // KHB_GATE_STAGE1_AUTO: an L2-sized 2 MiB fold of a gate of up to 32 MiB (k = 1: -6.4 % time,
-  // profiles/r04g_k1/ab.txt), a 32 MiB fold of a larger one (k = 4: 128 MiB beside the 57.5 MiB L1 bloom,
-  // where a 4 MiB fold measured 3.5 % slower and 8 / 16 MiB the same, profiles/r04g_k1/k4.txt)
-  const uint32_t f_log2 = c->gate1_log2 != KHB_GATE_STAGE1_AUTO ? c->gate1_log2 : bytes <= (1u << 25) ? 21u : 25u;
+  // KHB_GATE_STAGE1_AUTO: an L2-sized 2 MiB fold of a gate of up to 32 MiB (k = 1: -8.6 % time with two
+  // launches in flight, profiles/r04k/stage1_k1_nt_pipe_ab.txt), a 16 MiB fold of a larger one (k = 4: the
+  // 128 MiB gate beside the 57.5 MiB L1 bloom; 16 and 8 MiB -3.5 % vs 32 MiB with the non-temporal prefix
+  // stream, 4 MiB slower, profiles/r04l/k4_stage1_ab.txt)
+  const uint32_t f_log2 = c->gate1_log2 != KHB_GATE_STAGE1_AUTO ? c->gate1_log2 : bytes <= (1u << 25) ? 21u : 24u;
   if (f_log2 && (size_t)1 << f_log2 < bytes) {
     // stage 1: the gate OR-folded to 2^f_log2 bytes (a superset: no member is ever dropped)
     const size_t nb1 = ((size_t)1 << f_log2) / 8, nb = bytes / 8;

@@ -239,7 +239,7 @@ def test_k4_full_geometry_candidates_match_oracle(tables_k4, ora):
         # the product gate at k = 4 (2^30 bits, 128 MiB) with and without its 32 MiB stage-1 fold
         gate, lg = tables_k4.gate()
         gated = {}
-        for stage1 in (0, 25, 1):              # 1 = KHB_GATE_STAGE1_AUTO (32 MiB at k = 4)
+        for stage1 in (0, 25, 1):              # 1 = KHB_GATE_STAGE1_AUTO (16 MiB at k = 4)
             e.set_gate_stage1(stage1)
             e.load_gate(gate, lg, tables_k4.gate_probes())
             gated[stage1], gdegen, _ = e.scan(centres, 0, tables_k4.cycles)
