@@ -103,6 +103,15 @@ int khh_session_set_test_hooks(khh_session* s, uint32_t cand_cap, int use_gate, 
 #define KHH_CHECK_DEVICE 1
 #define KHH_CHECK_AUTO 2
 int khh_session_set_check_mode(khh_session* s, int mode);
+/* keyhunt's -B mode for later runs (keyhunt.cpp:227): 0 sequential, 1 backward, 2 both, 3 random, 4 dance
+ * (the thread_process_bsgs* variants, 3778-5700; engine.hpp ChunkCursor).  A run's random_chunks != 0
+ * still selects random. */
+int khh_session_set_chunk_mode(khh_session* s, int mode);
+/* The chunk bases a -B mode claims from [start, end) with chunks of two_n keys, in claim order, up to cap
+ * (out: 32 B BE each); the seed drives both / dance.  Returns the count (the whole sequence unless cap is
+ * reached or the mode is random).  Host only: the claim order the search uses. */
+uint64_t khh_chunk_sequence(int mode, const uint8_t start_be[32], const uint8_t end_be[32], const uint8_t two_n_be[32],
+                            uint64_t seed, uint8_t* out_be, uint64_t cap);
 /* Secp256K1::Init's GTable (secp256k1/SECP256K1.cpp:43-54), 32*256 points x||y BE (khb_check_tables.gtable). */
 void khh_gtable(uint8_t out[32 * 256 * 64]);
 /* Candidates recorded in the last run: chunk base (32 B BE), target index, giant step a; returns the

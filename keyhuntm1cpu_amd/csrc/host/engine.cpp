@@ -9,11 +9,58 @@
 #include <chrono>
 #include <deque>
 #include <mutex>
+#include <random>
 #include <thread>
 
 #include "../../../include/khbsgs.h"
 
 namespace khb {
+
+ChunkCursor::ChunkCursor(int mode, const U256& start, const U256& end, const U256& two_n, uint64_t seed)
+    : mode_(mode), start_(start), end_(end), two_n_(two_n), cursor_(start), top_(end), rng_(seed) {}
+
+// The next chunk from the top: keyhunt's `n_range_end -= 2N; base = max(n_range_end, lower)` while
+// n_range_end > lower (keyhunt.cpp:5122-5133 backward with lower = the range start; 5383-5400 both and
+// 4837-4854 dance with lower = BSGS_CURRENT).  Unsigned: a step to or below `lower` clamps to it and ends
+// the side, as the reference's next `n_range_end > lower` test does.
+bool ChunkCursor::top(const U256& lower, U256& base) {
+  if (!(top_ > lower)) return false;
+  if (top_ - lower <= two_n_) {
+    base = lower;
+    top_ = lower;
+  } else {
+    top_ = top_ - two_n_;
+    base = top_;
+  }
+  return true;
+}
+
+// The next chunk from the bottom (keyhunt.cpp:3843-3844; 5401-5414 both and 4855-4868 dance, n_range_end
+// moving).
+bool ChunkCursor::bottom(const U256& upper, U256& base) {
+  if (!(cursor_ < upper)) return false;
+  base = cursor_;
+  cursor_ = cursor_ + two_n_;
+  return true;
+}
+
+bool ChunkCursor::next(U256& base) {
+  switch (mode_) {
+    case kChunkRandom: base = random_in(start_, end_); return true;        // keyhunt.cpp:4069
+    case kChunkBackward: return top(start_, base);
+    case kChunkBoth: return rng_() % 2 ? bottom(top_, base) : top(cursor_, base);
+    case kChunkDance:
+      switch (rng_() % 3) {
+        case 0: return top(cursor_, base);
+        case 1: return bottom(top_, base);
+        default:                                   // base_key.Rand(&BSGS_CURRENT, &n_range_end), 4869-4870
+          if (!(cursor_ < top_)) return false;
+          base = random_in(cursor_, top_);
+          return true;
+      }
+    default: return bottom(end_, base);            // sequential, keyhunt.cpp:3843-3844
+  }
+}
 
 namespace {
 
@@ -44,7 +91,8 @@ struct Shared {
   const std::vector<Target>& targets;
   const SearchConfig& cfg;
   const SearchCallbacks& cb;
-  U256 start, end, cursor;
+  U256 start, end;
+  ChunkCursor chunks;       // the shared chunk cursor (keyhunt's BSGS_CURRENT / n_range_end)
   std::mutex mu;            // cursor, found, keys, stats, callbacks
   std::vector<int>& found;
   std::vector<U256>& keys;
@@ -125,13 +173,7 @@ bool claim(Shared& S, uint32_t want, Batch& b) {
   for (uint32_t i = 0; i < want && !S.stop; ++i) {
     if (S.cfg.max_chunks && S.claimed >= S.cfg.max_chunks) break;
     U256 base;
-    if (S.cfg.random_chunks) {
-      base = random_in(S.start, S.end);
-    } else {
-      base = S.cursor;
-      if (base >= S.end) break;            // keyhunt.cpp:3843-3844
-      S.cursor = S.cursor + S.T.geo.N_double;
-    }
+    if (!S.chunks.next(base)) break;
     b.bases.push_back(base);
     S.claimed++;
     if (S.cb.on_chunk) S.cb.on_chunk(base);
@@ -172,11 +214,17 @@ void job_centres(const Tables& T, const std::vector<U256>& bases, const std::vec
   const size_t nc = bases.size(), nt = tp.size();
   if (nc == 0 || nt == 0) return;
   std::vector<Pt> aux(nc);
-  bool consecutive = nc > 1;
-  for (size_t c = 1; c < nc && consecutive; ++c) consecutive = bases[c] == bases[c - 1] + T.geo.N_double;
-  if (consecutive)
+  bool up = nc > 1, down = nc > 1;
+  for (size_t c = 1; c < nc && (up || down); ++c) {
+    up = up && bases[c] == bases[c - 1] + T.geo.N_double;
+    down = down && bases[c - 1] == bases[c] + T.geo.N_double;     // -B backward claims descend
+  }
+  if (up) {
     T.chunk_aux_run(bases[0], nc, aux.data(), threads);
-  else
+  } else if (down) {
+    T.chunk_aux_run(bases[nc - 1], nc, aux.data(), threads);
+    std::reverse(aux.begin(), aux.end());
+  } else
     parallel_for(nc, threads, [&](size_t c) { aux[c] = T.chunk_aux(bases[c]); });
   constexpr size_t kJobBlock = 256;
   const size_t nj = nc * nt;
@@ -524,7 +572,9 @@ int Session::run(const std::vector<Target>& targets, const U256& start, const U2
   Shared S(*T_, targets, cfg, cb, found, keys, stats);
   S.start = start;
   S.end = end;
-  S.cursor = start;
+  uint64_t seed = 0;
+  if (getrandom(&seed, sizeof seed, 0) != (ssize_t)sizeof seed) seed = (uint64_t)time(nullptr);
+  S.chunks = ChunkCursor(cfg.random_chunks ? kChunkRandom : cfg.chunk_mode, start, end, T_->geo.N_double, seed);
   std::vector<std::thread> th;
   for (void* c : ctx_) th.emplace_back(device_thread, std::ref(S), (khb_ctx*)c);
   for (auto& t : th) t.join();

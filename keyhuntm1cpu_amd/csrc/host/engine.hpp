@@ -9,6 +9,7 @@
 #pragma once
 #include <stdint.h>
 #include <functional>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -35,6 +36,9 @@ struct SearchConfig {
   int check_threads = 0;           // CPU confirmation pool, 0 = auto
   uint64_t max_chunks = 0;         // 0 = until range end
   bool random_chunks = false;      // -B random: every chunk base drawn uniformly in the range
+  // keyhunt's -B mode (keyhunt.cpp:227 bsgs_modes, the thread_process_bsgs* variants 3778-5700): how chunk
+  // bases are claimed.  kChunkRandom is also selected by random_chunks.
+  int chunk_mode = 0;
   bool use_gate = true;            // load the tables' level-0 gate (khb_load_gate) when they have one
   int queue_depth = 2;             // batches queued per device (1 or 2; 2 overlaps launch tails)
   uint32_t cand_cap = 0;           // candidate ring entries per launch (0 = library default, 2^20); tests
@@ -47,9 +51,31 @@ struct SearchConfig {
   int check_mode = 0;
 };
 enum : int { kCheckHost = 0, kCheckDevice = 1, kCheckAuto = 2 };
+// -B modes in keyhunt's order: sequential (thread_process_bsgs, 3824-3844: a cursor from the range start up
+// by 2N), backward (5072-5325: from the range end down by 2N, the last chunk clamped to the start), both
+// (5329-5700: each claim from the top or the bottom at random until they meet), random (4014-4264: a
+// uniform base in the range), dance (4794-5068: top, bottom or a uniform base between them, at random).
+enum : int { kChunkSequential = 0, kChunkBackward = 1, kChunkBoth = 2, kChunkRandom = 3, kChunkDance = 4 };
 constexpr uint32_t kCheckAutoMin = 4096;
 // The --check argument of keyhunt_amd / bsgsd_amd: "host", "gpu" or "auto"; -1 for anything else.
 int parse_check_mode(const char* s);
+
+// The chunk bases of one search in claim order (keyhunt's BSGS_CURRENT / n_range_end under bsgs_thread),
+// for a -B mode (kChunk*); the seed drives the both / dance side choices.  Shared by every device thread
+// under the engine's lock.
+class ChunkCursor {
+ public:
+  ChunkCursor() = default;
+  ChunkCursor(int mode, const U256& start, const U256& end, const U256& two_n, uint64_t seed);
+  bool next(U256& base);     // false when the mode's range is exhausted (random: never)
+
+ private:
+  bool top(const U256& lower, U256& base);
+  bool bottom(const U256& upper, U256& base);
+  int mode_ = kChunkSequential;
+  U256 start_, end_, two_n_, cursor_, top_;
+  std::mt19937_64 rng_;
+};
 
 struct SearchStats {
   uint64_t launches = 0;           // GPU scan launches (one per batch per device)

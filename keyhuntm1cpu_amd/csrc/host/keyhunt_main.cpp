@@ -38,7 +38,7 @@ const char* kLimitPrefix[7] = {"Mkeys/s", "Gkeys/s", "Tkeys/s", "Pkeys/s", "Ekey
 void menu() {
   printf("\nUsage:\n");
   printf("-h          show this help\n");
-  printf("-B Mode     BSGS now have some modes <sequential, random> (backward, both, dance: not yet)\n");
+  printf("-B Mode     BSGS now have some modes <sequential, backward, both, random, dance>\n");
   printf("-b bits     For some puzzles you only need some numbers of bits in the test keys.\n");
   printf("-f file     Specify file name with public keys (02/03 compressed or 04 uncompressed hex)\n");
   printf("-k value    Use this only with bsgs mode, k value is factor for M, more speed but more RAM use wisely\n");
@@ -277,6 +277,15 @@ int main(int argc, char** argv) {
         exit(EXIT_FAILURE);
     }
   }
+  // keyhunt.cpp:780-789: compared with MODE_BSGS (2), i.e. the -B sub-mode "both", whatever -m is
+  if (bsgs_mode == 2 && endomorphism) {
+    fprintf(stderr, "[E] Endomorphism doesn't work with BSGS\n");
+    exit(EXIT_FAILURE);
+  }
+  if (bsgs_mode == 2 && ao.stride) {
+    fprintf(stderr, "[E] Stride doesn't work with BSGS\n");
+    exit(EXIT_FAILURE);
+  }
   if (mode == 1 || mode == 3) {
     if (eth) {
       fprintf(stderr, "[E] keyhunt_amd searches BTC P2PKH addresses only (-c eth is not available)\n");
@@ -328,15 +337,11 @@ int main(int argc, char** argv) {
             kModes[mode]);
     exit(EXIT_FAILURE);
   }
-  // keyhunt.cpp:780-789 reject -e / -I only for the BSGS sub-mode "both" (they compare the sub-mode
-  // with MODE_BSGS); that sub-mode is refused below, so -e / -I are ignored here as there.
-  if (bsgs_mode != 0 && bsgs_mode != 3) {
-    fprintf(stderr, "[E] BSGS mode %s is not implemented by keyhunt_amd yet\n", kBsgsModes[bsgs_mode]);
-    exit(EXIT_FAILURE);
-  }
+  // -e / -I outside the sub-mode "both" are ignored by -m bsgs, as there (keyhunt.cpp:780-789 above)
   printf("[+] Mode BSGS %s\n", kBsgsModes[bsgs_mode]);
   if (!file) file = "addresses.txt";   // default_fileName, keyhunt.cpp:231
   if (gpu_blocks) cfg.lanes = gpu_blocks * 256u;
+  cfg.chunk_mode = bsgs_mode;                       // sequential, backward, both, random, dance
   cfg.random_chunks = bsgs_mode == 3;
   cfg.check_threads = nthreads;
 

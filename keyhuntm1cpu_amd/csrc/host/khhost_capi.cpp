@@ -253,6 +253,27 @@ int khh_session_set_check_mode(khh_session* s, int mode) {
   return s->s.set_check_mode(mode);
 }
 
+int khh_session_set_chunk_mode(khh_session* s, int mode) {
+  if (!s || mode < kChunkSequential || mode > kChunkDance) return KHB_EINVAL;
+  s->s.config().chunk_mode = mode;
+  return 0;
+}
+
+uint64_t khh_chunk_sequence(int mode, const uint8_t start_be[32], const uint8_t end_be[32], const uint8_t two_n_be[32],
+                            uint64_t seed, uint8_t* out_be, uint64_t cap) {
+  if (mode < kChunkSequential || mode > kChunkDance) return 0;
+  const U256 two_n = U256::from_be(two_n_be);
+  if (two_n == U256()) return 0;
+  ChunkCursor c(mode, U256::from_be(start_be), U256::from_be(end_be), two_n, seed);
+  uint64_t n = 0;
+  U256 base;
+  while (n < cap && c.next(base)) {
+    if (out_be) base.to_be(out_be + 32 * n);
+    n++;
+  }
+  return n;
+}
+
 void khh_gtable(uint8_t out[32 * 256 * 64]) {
   const std::vector<uint8_t>& g = gtable_be();
   memcpy(out, g.data(), g.size());

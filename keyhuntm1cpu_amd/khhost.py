@@ -70,6 +70,10 @@ def lib() -> C.CDLL:
         L.khh_session_close.argtypes = [C.c_void_p]
         L.khh_session_set_test_hooks.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_char_p]
         L.khh_session_set_check_mode.argtypes = [C.c_void_p, C.c_int]
+        L.khh_session_set_chunk_mode.argtypes = [C.c_void_p, C.c_int]
+        L.khh_chunk_sequence.restype = C.c_uint64
+        L.khh_chunk_sequence.argtypes = [C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint64, C.c_char_p,
+                                         C.c_uint64]
         L.khh_gtable.argtypes = [C.c_char_p]
         L.khh_session_recorded.restype = C.c_uint64
         L.khh_session_recorded.argtypes = [C.c_void_p, C.c_char_p, P(C.c_uint32), P(C.c_uint32), C.c_uint64]
@@ -259,6 +263,14 @@ class Tables:
 _STAT_KEYS = ("chunks", "giant_steps", "candidates", "degenerate", "kernel_s", "launches", "rescans", "busy_s",
               "shader_mhz", "device_checked", "device_check_s")
 CHECK_HOST, CHECK_DEVICE, CHECK_AUTO = 0, 1, 2      # include/khhost.h KHH_CHECK_*
+BSGS_MODES = ("sequential", "backward", "both", "random", "dance")     # keyhunt.cpp:227, -B
+
+
+def chunk_sequence(mode: int, start: int, end: int, two_n: int, seed: int = 1, cap: int = 1 << 16) -> list[int]:
+    """The chunk bases -B mode `mode` claims from [start, end) (khh_chunk_sequence; the engine's order)."""
+    out = C.create_string_buffer(32 * cap)
+    n = lib().khh_chunk_sequence(mode, _b32(start), _b32(end), _b32(two_n), seed, out, cap)
+    return [int.from_bytes(out.raw[32 * i:32 * i + 32], "big") for i in range(n)]
 
 
 def gtable() -> bytes:
@@ -308,6 +320,12 @@ class Session:
         st["shader_mhz"] = stats[8] / 1e3
         st["device_check_s"] = stats[10] / 1e6
         return res, st
+
+    def set_chunk_mode(self, mode: int) -> None:
+        """keyhunt's -B mode for later runs: BSGS_MODES.index(name) (0 sequential ... 4 dance)."""
+        rc = lib().khh_session_set_chunk_mode(self.h, mode)
+        if rc:
+            raise KhhError(f"set_chunk_mode failed ({rc})")
 
     def set_check_mode(self, mode: int) -> None:
         """Where later runs confirm candidates: CHECK_HOST (CPU pool), CHECK_DEVICE (khb_check), CHECK_AUTO."""

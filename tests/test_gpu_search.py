@@ -301,3 +301,46 @@ def test_random_chunk_mode_finds_the_key(keys):
         assert 1 <= st["chunks"] <= 40
     finally:
         t.close()
+
+
+@pytest.mark.parametrize("mode", ["backward", "both", "dance"])
+def test_bsgs_modes_find_keys(mode):
+    """keyhunt's -B backward / both / dance (keyhunt.cpp:4794-5700) through the product session: keys near
+    either end of the range are found; backward reaches the key near the end in its first chunks."""
+    t = khhost.Tables(hex(1 << 24), 1, threads=8)         # 2N = 2^25 keys per chunk
+    two_n = 2 * t.n_low
+    start = 1 << 44
+    end = start + 512 * two_n
+    lo_key, hi_key = start + 3 * two_n + 0x1234, end - 2 * two_n - 0x777
+    with khhost.Session(t) as s:
+        s.set_chunk_mode(khhost.BSGS_MODES.index(mode))
+        res, st = s.run([khhost.pubkey(lo_key), khhost.pubkey(hi_key)], start, end)
+    assert res == [lo_key, hi_key]
+    if mode == "backward":
+        # the whole range is claimed from the top; the low key is found last
+        assert st["chunks"] >= 509
+
+
+def test_bsgs_backward_covers_range_once():
+    """-B backward over a range of 100.5 chunks with no key in it: 101 chunks claimed (the last one clamped to
+    the range start, keyhunt.cpp:5124-5125), device-counted giant steps = chunks x cycles x 1024."""
+    t = khhost.Tables(hex(1 << 24), 1, threads=8)
+    two_n = 2 * t.n_low
+    start = 1 << 45
+    end = start + 100 * two_n + two_n // 2
+    with khhost.Session(t) as s:
+        s.set_chunk_mode(1)
+        res, st = s.run([khhost.pubkey(0x123456789)], start, end)
+    assert res == [None]
+    assert st["chunks"] == 101
+    assert st["giant_steps"] == 101 * t.cycles * 1024
+
+
+def test_cli_bsgs_backward_known_answer(tmp_path):
+    p30 = "030d282cf2ff536d2c42f105d0b8588821a915dc3f9a05bd98bb23af67a2e92a5b"
+    (tmp_path / "30.pub").write_text(p30 + "\n")
+    r = _cli(["-m", "bsgs", "-B", "backward", "-f", "30.pub", "-b", "30", "-n", "0x100000", "-q", "-s", "0"], tmp_path)
+    assert r.returncode == 1, r.stdout + r.stderr
+    assert "[+] Mode BSGS backward" in r.stdout and "privkey 3d94cd64" in r.stdout
+    r = _cli(["-m", "bsgs", "-B", "both", "-e", "-f", "30.pub", "-b", "30"], tmp_path)
+    assert r.returncode == 1 and "Endomorphism doesn't work with BSGS" in r.stderr
