@@ -289,11 +289,18 @@ int confirm(Shared& S, khb_ctx* ctx, const Batch& b, std::vector<khb_cand>& cand
     std::lock_guard<std::mutex> lk(S.mu);
     found_snapshot = S.found;
   }
-  const bool dev = S.cfg.check_mode == kCheckDevice || (S.cfg.check_mode == kCheckAuto && cands.size() > kCheckAutoMin);
+  bool dev = S.cfg.check_mode == kCheckDevice || (S.cfg.check_mode == kCheckAuto && cands.size() > kCheckAutoMin);
   if (dev) {
     const int rc = confirm_device(S, ctx, b, cands, found_snapshot, ok, key);
-    if (rc) return rc;
-  } else {
+    if (rc) {      // the host pool confirms this batch instead (the same keys); the search goes on
+      std::lock_guard<std::mutex> lk(S.mu);
+      if (S.cb.on_warning)
+        S.cb.on_warning(std::string("[W] device check failed (") + khb_strerror(rc) + "): this batch is confirmed on the host");
+      std::fill(ok.begin(), ok.end(), 0);
+      dev = false;
+    }
+  }
+  if (!dev) {
     parallel_for(cands.size(), threads, [&](size_t i) {
       const uint32_t job = cands[i].job;
       const uint32_t k = b.job_target[job];
