@@ -3,8 +3,8 @@
 
 --workload p66 (default; BASELINE.json configs[1], -b 66, k=1; --k 4 = configs[2]):
   one step = one GPU scan batch of the product search (libkhhost -> libkhbsgs): host centres for
-  3072 chunks, the HIP giant-step kernel over all 4096 groups of each chunk (1.5 x 2^33 giant steps:
-  eight 8-group work items per lane of a full residency of 196,608 lanes at 3 waves/SIMD, as the CLI's
+  4096 chunks, the HIP giant-step kernel over all 4096 groups of each chunk (2^34 giant steps:
+  eight 8-group work items per lane of a full residency of 262,144 lanes at 4 waves/SIMD, as the CLI's
   auto batch), and the CPU confirmation
   of every candidate, pipelined exactly as the keyhunt_amd CLI runs it.  The -b 66 range [2^65, 2^66)
   is partitioned statically into one contiguous chunk block per rank (partition.key_block, north_star);
@@ -222,7 +222,7 @@ def main():
     fill = -(-khbsgs.default_lanes(local) * khbsgs.groups_per_item() // tables.cycles)
     if auto_chunks:
         # eight work items per lane, as the CLI's auto batch (engine.cpp batch_chunks): waves take
-        # items dynamically (KHB_DYN), so a deeper queue keeps every SIMD 3 waves deep until the
+        # items dynamically (KHB_DYN), so a deeper queue keeps every SIMD 4 waves deep until the
         # launch's last items (profiles/r01c_dyn_probe.txt)
         args.chunks = max(1, (1 << 30) // (tables.cycles * 1024), 8 * fill)
     two_n = 2 * (tables.n_low)                     # 2N keys per chunk

@@ -96,7 +96,7 @@ uint32_t khb_default_lanes(int device);
  * when n_jobs * ceil(group_count / khb_groups_per_item()) >= khb_lanes(ctx). */
 uint32_t khb_groups_per_item(void);
 /* Allocate the device state of the first `depth` submission slots now (1 or 2; a slot's prefix scratch
- * is 4,120 x 32 B x khb_lanes(ctx): ~26 GB at the auto 196,608 lanes on MI355X) instead of on the first queued submission.  KHB_ENOMEM leaves the
+ * is 4,120 x 32 B x khb_lanes(ctx): ~35 GB at the auto 262,144 lanes on MI355X) instead of on the first queued submission.  KHB_ENOMEM leaves the
  * extra slot empty and the context usable with one submission in flight (the caller's queue depth 1). */
 int khb_reserve_slots(khb_ctx* ctx, int depth);
 /* Candidate ring entries a -m bsgs launch keeps (default and maximum 2^20).  Lowering it is for tests

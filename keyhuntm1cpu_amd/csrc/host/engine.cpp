@@ -358,7 +358,7 @@ void device_thread(Shared& S, khb_ctx* ctx) {
                                                : (int)std::max(2u, std::min(16u, std::thread::hardware_concurrency()));
   int depth = std::max(1, std::min(S.cfg.queue_depth, 2));
   if (depth > 1) {
-    // the second slot's scratch (~26 GB at the default lanes) up front; without it the device runs one
+    // the second slot's scratch (~35 GB at the default lanes) up front; without it the device runs one
     // batch at a time
     const int rrc = khb_reserve_slots(ctx, depth);
     if (rrc == KHB_ENOMEM) {

@@ -32,10 +32,12 @@ struct AffPt {
 #define KHB_GATE1 1               // default stage-1 fold of the level-0 gate: KHB_GATE_STAGE1_AUTO (khbsgs.h)
 #endif
 #ifndef KHB_WAVES_PER_SIMD
-// occupancy target of k_giant_scan (launch bounds).  Round 3: 3 waves/SIMD (168 VGPRs, 196,608 lanes)
-// ran 1.4-1.6 % faster than 4 (128 VGPRs) in two A/B runs, 2 waves 6 % slower
-// (profiles/r03_calibration/occupancy_ab*.txt); round 1 had measured 3 and 4 equal.
-#define KHB_WAVES_PER_SIMD 3
+// occupancy target of k_giant_scan (launch bounds).  Round 4: 4 waves/SIMD (128 VGPRs, 262,144 lanes; the walk's
+// hot path has the same 1,171 VALU per step as at 3 waves) ran 3.0 % faster than 3 (168 VGPRs) with two
+// launches in flight, at 3,072 and at 4,096 chunks per launch, and 5 waves (96 VGPRs, spilling) 16 % slower
+// (profiles/r04q/waves_pipe_ab.txt).  Round 3, before the L2 gate fold and the non-temporal prefix stream,
+// had measured 3 waves 1.4-1.6 % faster than 4 (profiles/r03_calibration/occupancy_ab*.txt).
+#define KHB_WAVES_PER_SIMD 4
 #endif
 constexpr uint32_t kBlock = 256;
 #ifndef KHB_BATCH
