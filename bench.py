@@ -370,8 +370,14 @@ def main():
         try:
             with open(pmc_path) as f:
                 pmc = json.load(f)
-            if pmc.get("chunks_per_launch") == args.chunks and pmc.get("k") == args.k:
-                roofline["traffic"] = pmc.get("hbm_bytes_per_launch")
+            if pmc.get("k") == args.k:
+                if pmc.get("chunks_per_launch") == args.chunks:
+                    roofline["traffic"] = pmc.get("hbm_bytes_per_launch")
+                else:
+                    # another batch than the PMC launch's: the per-giant-step bytes at this launch's size
+                    roofline["traffic"] = int(round(pmc["bytes_per_giant_step"] * per_launch_steps))
+                    roofline["traffic_note"] = ("PMC bytes per giant step measured at %d chunks per launch, "
+                                                "scaled to %d" % (pmc["chunks_per_launch"], args.chunks))
                 roofline["traffic_source"] = os.path.relpath(pmc_path, REPO)
                 if pmc.get("valu_instr_per_giant_step"):
                     vi = pmc["valu_instr_per_giant_step"]

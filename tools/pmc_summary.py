@@ -1,4 +1,4 @@
-"""profiles/pmc_latest.json from the PMC passes of tools/gpu/r03u.sh (bench.py reads it for
+"""profiles/pmc_latest.json from the PMC passes of tools/gpu/round_profile.sh (bench.py reads it for
 roofline.traffic and the executed VALU figures).
 
 Inputs (rocprofv3 --pmc CSVs, one timed k_giant_scan launch each, JOBS chunks of the default k=1
