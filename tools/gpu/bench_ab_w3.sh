@@ -1,3 +1,9 @@
+#!/bin/bash
+# Same-box bench A/B of the 4-wave product library against a 3-wave build (profiles/r04s): two interleaved
+# rounds of bench.py, the 3-wave library picked up by libkhhost through LD_LIBRARY_PATH (RUNPATH $ORIGIN
+# yields to it; maps.txt records which libkhbsgs.so was loaded).  Build the 3-wave library first:
+#   bash tools/build_variant.sh w3tmp -DKHB_WAVES_PER_SIMD=3 && mkdir -p keyhuntm1cpu_amd/lib/variants/w3 &&
+#   mv keyhuntm1cpu_amd/lib/variants/libkhbsgs_w3tmp.so keyhuntm1cpu_amd/lib/variants/w3/libkhbsgs.so
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r04s; mkdir -p $O
