@@ -59,6 +59,16 @@ PEAK_LANES_PER_CLK_CU, CUS = 57.8, 256
 PEAK_CLK_GHZ, MICROBENCH_CLK_GHZ = 2.4, 2.16
 
 
+def pmc_traffic(pmc: dict, chunks: int, launch_steps: int) -> dict:
+    """roofline.traffic for one launch of `chunks` chunks from profiles/pmc_latest.json: its measured bytes
+    when the PMC launch had the same size, else its bytes per giant step scaled to this launch (noted)."""
+    if pmc.get("chunks_per_launch") == chunks:
+        return {"traffic": pmc.get("hbm_bytes_per_launch")}
+    return {"traffic": int(round(pmc["bytes_per_giant_step"] * launch_steps)),
+            "traffic_note": "PMC bytes per giant step measured at %d chunks per launch, scaled to %d"
+                            % (pmc["chunks_per_launch"], chunks)}
+
+
 def mulops_peak_t(ghz: float) -> float:
     return round(PEAK_LANES_PER_CLK_CU * CUS * ghz * 1e9 / 1e12, 2)
 
@@ -371,13 +381,7 @@ def main():
             with open(pmc_path) as f:
                 pmc = json.load(f)
             if pmc.get("k") == args.k:
-                if pmc.get("chunks_per_launch") == args.chunks:
-                    roofline["traffic"] = pmc.get("hbm_bytes_per_launch")
-                else:
-                    # another batch than the PMC launch's: the per-giant-step bytes at this launch's size
-                    roofline["traffic"] = int(round(pmc["bytes_per_giant_step"] * per_launch_steps))
-                    roofline["traffic_note"] = ("PMC bytes per giant step measured at %d chunks per launch, "
-                                                "scaled to %d" % (pmc["chunks_per_launch"], args.chunks))
+                roofline.update(pmc_traffic(pmc, args.chunks, per_launch_steps))
                 roofline["traffic_source"] = os.path.relpath(pmc_path, REPO)
                 if pmc.get("valu_instr_per_giant_step"):
                     vi = pmc["valu_instr_per_giant_step"]

@@ -110,3 +110,21 @@ def test_committed_pmc_latest_reproduces_from_its_csvs(tmp_path):
               "valu_instr_per_giant_step"):
         assert again[k] == cur[k], k
     assert pmc_summary.GROUPS == 4096
+
+
+def test_bench_traffic_matches_default_batch():
+    """The committed PMC launch has the bench's auto batch at 4 waves/SIMD (8 work items per lane of 262,144
+    lanes: 4,096 chunks of the k=1 geometry), so the default line's roofline.traffic is the measured launch;
+    another --chunks scales the measured bytes per giant step and says so."""
+    sys.path.insert(0, REPO)
+    import bench
+    with open(os.path.join(REPO, "profiles", "pmc_latest.json")) as f:
+        pmc = json.load(f)
+    lanes, per_item, cycles = 4 * 4 * 64 * 256, 8, 4096
+    auto = 8 * (-(-lanes * per_item // cycles))
+    assert pmc["k"] == 1 and pmc["chunks_per_launch"] == auto == 4096
+    steps = auto * cycles * 1024
+    assert bench.pmc_traffic(pmc, auto, steps) == {"traffic": pmc["hbm_bytes_per_launch"]}
+    half = bench.pmc_traffic(pmc, auto // 2, steps // 2)
+    assert abs(half["traffic"] - pmc["hbm_bytes_per_launch"] / 2) < 1e-3 * pmc["hbm_bytes_per_launch"]
+    assert "scaled to 2048" in half["traffic_note"]
