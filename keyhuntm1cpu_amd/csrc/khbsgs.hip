@@ -505,6 +505,15 @@ int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t 
   c->gate_mask = c->gate1_mask = 0;
   if (!gate) return KHB_OK;
   const size_t bytes = (size_t)1 << (log2_bits - 3);
+  // one probe: every block's hi word set on the device copy, so the kernels' fixed three-probe test
+  // (scan_kernels.hpp gate_block_pass: probe 1 reads hi, probe 2 repeats probe 0) gives the one-probe answer
+  std::vector<uint64_t> one;
+  if (probes == 1) {
+    one.resize(bytes / 8);
+    memcpy(one.data(), gate, bytes);
+    for (uint64_t& b : one) b |= 0xFFFFFFFF00000000ull;
+    gate = reinterpret_cast<const uint8_t*>(one.data());
+  }
   KHB_TRY(c, hipMalloc(&c->d_gate, bytes));
   KHB_TRY(c, hipMemcpy(c->d_gate, gate, bytes, hipMemcpyHostToDevice));
   c->gate_mask = (uint32_t)((1ull << (log2_bits - 6)) - 1);

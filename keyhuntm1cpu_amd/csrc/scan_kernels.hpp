@@ -215,32 +215,33 @@ __device__ __forceinline__ void q_push(ProbeQueue& Q, bool hit, const Fe& x, uin
   *Q.n = n + (uint32_t)__popcll(m);
 }
 
-// The gate's bits in x's 64-bit block (lo, hi words): probe p tests bit (w1 >> 5p) mod 32 of word p mod 2
-// (p = 0: lo, 1: hi, 2: lo), w1 = x.v[1].  32-bit shifts take their amount mod 32 in hardware, so each
-// probe is one shift of a block word with no word select: the round-3 layout (6-bit positions in the
-// whole block) selected the word per probe with a v_cndmask_b32 on VCC.  Probes
-// beyond A.gate_probes are masked to "set" by wave-uniform words (no per-lane select either).
-struct GateMask {
-  uint32_t m1, m2;       // 1 when probe 1 / probe 2 is unused
+// The gate's bits in x's 64-bit block (lo, hi words): probe p tests bit b_p = (w1 >> 5p) mod 32 of word
+// p mod 2 (p = 0: lo, 1: hi, 2: lo), w1 = x.v[1].  Each probe is one left shift by 31 - b_p = (~w1 >> 5p)
+// mod 32 that brings its bit to bit 31 (the hardware takes a 32-bit shift's amount mod 32, so the amounts
+// need no mask and no word select); the block passes when the AND of the three shifted words is negative.
+// The amounts are computed once per x and shared by the stage-1 fold's test and the full gate's.  Fewer
+// probes than 3 need no per-lane masks: probe 2 repeats probe 0 (shift distance 0 instead of 10,
+// wave-uniform), and for one probe khb_load_gate sets every block's hi word, so probe 1 always passes.
+struct GateBits {
+  uint32_t a0, a1, a2;   // left-shift amounts (mod 32) of probes 0, 1, 2
 };
-__device__ __forceinline__ GateMask gate_mask(const ScanArgs& A) {
-  return GateMask{A.gate_probes < 2 ? 1u : 0u, A.gate_probes < 3 ? 1u : 0u};
+__device__ __forceinline__ uint32_t gate_s2(const ScanArgs& A) { return A.gate_probes >= 3 ? 10u : 0u; }
+__device__ __forceinline__ GateBits gate_bits(uint32_t w1, uint32_t s2) {
+  const uint32_t n = ~w1;
+  return GateBits{n, n >> 5, n >> s2};
 }
-__device__ __forceinline__ bool gate_block_pass(uint32_t lo, uint32_t hi, uint32_t w1, GateMask m) {
-  const uint32_t r = (lo >> (w1 & 31u)) & ((hi >> ((w1 >> 5) & 31u)) | m.m1) & ((lo >> ((w1 >> 10) & 31u)) | m.m2);
-  return r & 1u;
+// v_lshlrev_b32 as the hardware reads it (amount mod 32); opaque to the compiler, which otherwise masks
+// an amount computed in another basic block with a v_and_b32 (round-4 ISA of the fold's second test)
+__device__ __forceinline__ uint32_t shl_mod32(uint32_t x, uint32_t s) {
+  uint32_t r;
+  asm("v_lshlrev_b32 %0, %1, %2" : "=v"(r) : "v"(s), "v"(x));
+  return r;
 }
-
-// A gate test: x's 64-bit block of the map (one 8-byte load: a single cache line per x whatever the
-// probe count) and x's second word, which holds the bit positions.
-struct GatePend {
-  uint32_t lo, hi, w1;
-  __device__ __forceinline__ bool pass(GateMask m) const { return gate_block_pass(lo, hi, w1, m); }
-};
-
-__device__ __forceinline__ GatePend gate_issue(const ScanArgs& A, const Fe& x) {
-  const uint2 w = reinterpret_cast<const uint2*>(A.gate)[x.v[0] & A.gate_mask];
-  return GatePend{w.x, w.y, x.v[1]};
+__device__ __forceinline__ bool gate_block_pass(uint2 w, GateBits b) {
+  return (int32_t)(shl_mod32(w.x, b.a0) & shl_mod32(w.y, b.a1) & shl_mod32(w.x, b.a2)) < 0;
+}
+__device__ __forceinline__ uint2 gate_block(const uint8_t* g, uint32_t mask, const Fe& x) {
+  return reinterpret_cast<const uint2*>(g)[x.v[0] & mask];
 }
 
 // kScanG: gate test of one walk step's two x (x2 absent at step 511: has2 = false, uniform).  Both
@@ -249,22 +250,22 @@ template <bool STAGE1>
 __device__ __forceinline__ void gate_pair(const ScanArgs& A, ProbeQueue& Q, const Fe& x1, uint32_t step1, bool has2,
                                           const Fe& x2, uint32_t step2, uint32_t job) {
   bool h1, h2;
-  const GateMask gm = gate_mask(A);
+  const uint32_t s2 = gate_s2(A);
+  const GateBits b1 = gate_bits(x1.v[1], s2), b2 = gate_bits(x2.v[1], s2);
   if constexpr (STAGE1) {
     // stage 1 (L2-resident fold); the full gate's line is fetched only for its survivors
-    const uint2 f1 = reinterpret_cast<const uint2*>(A.gate1)[x1.v[0] & A.gate1_mask];
-    const uint2 f2 = reinterpret_cast<const uint2*>(A.gate1)[x2.v[0] & A.gate1_mask];
-    const bool s1 = gate_block_pass(f1.x, f1.y, x1.v[1], gm), s2 = has2 && gate_block_pass(f2.x, f2.y, x2.v[1], gm);
-    if (__ballot(s1 || s2) == 0) return;
-    uint2 w1 = make_uint2(0u, 0u), w2 = make_uint2(0u, 0u);
-    if (s1) w1 = reinterpret_cast<const uint2*>(A.gate)[x1.v[0] & A.gate_mask];
-    if (s2) w2 = reinterpret_cast<const uint2*>(A.gate)[x2.v[0] & A.gate_mask];
-    h1 = s1 && gate_block_pass(w1.x, w1.y, x1.v[1], gm);
-    h2 = s2 && gate_block_pass(w2.x, w2.y, x2.v[1], gm);
+    const uint2 f1 = gate_block(A.gate1, A.gate1_mask, x1), f2 = gate_block(A.gate1, A.gate1_mask, x2);
+    const bool s1 = gate_block_pass(f1, b1), s2p = has2 && gate_block_pass(f2, b2);
+    if (__ballot(s1 || s2p) == 0) return;
+    uint2 w1, w2;                                  // read only where loaded (s1 / s2p)
+    if (s1) w1 = gate_block(A.gate, A.gate_mask, x1);
+    if (s2p) w2 = gate_block(A.gate, A.gate_mask, x2);
+    h1 = s1 && gate_block_pass(w1, b1);
+    h2 = s2p && gate_block_pass(w2, b2);
   } else {
-    const GatePend q1 = gate_issue(A, x1), q2 = gate_issue(A, x2);
-    h1 = q1.pass(gm);
-    h2 = has2 && q2.pass(gm);
+    const uint2 w1 = gate_block(A.gate, A.gate_mask, x1), w2 = gate_block(A.gate, A.gate_mask, x2);
+    h1 = gate_block_pass(w1, b1);
+    h2 = has2 && gate_block_pass(w2, b2);
   }
   if (__ballot(h1 || h2) == 0) return;
   q_push(Q, h1, x1, job, step1);
@@ -277,8 +278,7 @@ __device__ __forceinline__ void gate_pair(const ScanArgs& A, ProbeQueue& Q, cons
 __device__ __forceinline__ bool first_bit(const ScanArgs& A, const Fe& x, uint64_t& a) {
   if (A.gate) {
     a = 0;
-    const uint2 w = reinterpret_cast<const uint2*>(A.gate)[x.v[0] & A.gate_mask];
-    return gate_block_pass(w.x, w.y, x.v[1], gate_mask(A));
+    return gate_block_pass(gate_block(A.gate, A.gate_mask, x), gate_bits(x.v[1], gate_s2(A)));
   }
   uint64_t w[4];
   x_words(w, x);

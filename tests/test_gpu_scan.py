@@ -199,7 +199,7 @@ def _l1_check(bf: bytes, nb: int, bits: int, hashes: int, xb: bytes, ora) -> boo
     return True
 
 
-@pytest.mark.parametrize("probes", [1, 3])
+@pytest.mark.parametrize("probes", [1, 2, 3])
 def test_gate_candidates_exact(eng, bs32, ora, probes):
     """Level-0 gate (khb_load_gate): the candidates are exactly the giant steps whose x passes the
     level-1 bloom AND whose gate bits (helpers.gate_bits: one 64-bit block, `probes` bits in it)
