@@ -95,7 +95,7 @@ def test_p66_batch_shrinks_to_fit(world):
     """bench.py's auto batch for a long run: shrunk to whole work items per lane so that every rank's
     W + K steps stay inside its -b 66 block; unchanged when it fits; refused (0) below one item per lane."""
     from keyhuntm1cpu_amd.partition import blocks_fit, fit_batch
-    fill = 384                                     # 196,608 lanes x 8 groups / 4096 groups per chunk
+    fill = 512                                     # 262,144 lanes x 8 groups / 4096 groups per chunk
     assert fit_batch(LO, HI, TWO_N, world, 25, 8 * fill, fill, P66_KEY) == 8 * fill
     for steps in (105, 300):
         c = fit_batch(LO, HI, TWO_N, world, steps, 8 * fill, fill, P66_KEY)
@@ -107,3 +107,11 @@ def test_p66_batch_shrinks_to_fit(world):
         else:
             assert not all(ok for _, _, ok in blocks_fit(LO, HI, TWO_N, world, steps * fill, P66_KEY))
     assert fit_batch(LO, HI, TWO_N, world, 5000, 8 * fill, fill, P66_KEY) == 0
+
+
+def test_p66_default_run_batches():
+    """The driver's default run (100 timed + 5 warmup steps) at the 4-wave auto batch: 4,096 chunks per
+    step at N = 1, shrunk to 2,048 / 2,048 / 1,024 at N = 2 / 4 / 8 (profiles/r04y measured
+    those batch sizes at the same per-GPU rate)."""
+    from keyhuntm1cpu_amd.partition import fit_batch
+    assert [fit_batch(LO, HI, TWO_N, w, 105, 4096, 512, P66_KEY) for w in (1, 2, 4, 8)] == [4096, 2048, 2048, 1024]
