@@ -42,7 +42,7 @@ if int(os.environ.get("GATE_ZERO", "0") or 0):
     lz = int(os.environ["GATE_ZERO"])
     gates[-lz] = bytes((1 << lz) // 8)
     gsets.append(-lz)
-# One Engine at a time: each owns ~26 GB of scratch per submission slot, so every (variant, gate) pair
+# One Engine at a time: each owns ~35 GB of scratch per submission slot (262,144 lanes), so every (variant, gate) pair
 # gets its own context per round, opened, timed and closed before the next one (round 3 kept all of them
 # open at once and ran out of HBM with six variants, gpurun_out/r03m/ab.txt).
 # STAGE1=default,0,22: time every real gate with the library's default stage-1 fold (KHB_GATE_STAGE1_AUTO),
