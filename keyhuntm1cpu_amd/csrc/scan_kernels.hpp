@@ -75,7 +75,7 @@ constexpr size_t kCounterBytes = 64;                 // ScanArgs::counters
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 // Prefix-scratch stream (written once by the forward pass, read once by the walk ~512 steps later, from
-// HBM: 26 GB per slot).  Non-temporal loads and stores keep it from displacing the level-0 gate's L2-sized
+// HBM: ~35 GB per slot at 262,144 lanes).  Non-temporal loads and stores keep it from displacing the level-0 gate's L2-sized
 // stage-1 fold (khb_set_gate_stage1): -1.5 % time with two launches in flight, -0.3 % as one launch
 // (profiles/r04i/nt_ab.txt, r04h/ntall_ab.txt).  Without the fold (round 1, 4 waves/SIMD) they measured
 // slower (profiles/r01_gate_experiments_raw.txt); tools/experiments/plainscr_patch.py builds the plain form.
