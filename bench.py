@@ -133,6 +133,18 @@ def cpu_baseline(seconds: float, threads: int, target, base: int):
     return steps / el
 
 
+def power_sampler(torch, local: int, args):
+    """Board power / clock sampler over the timed region (keyhuntm1cpu_amd/power.py; amdsmi, not HIP)."""
+    from keyhuntm1cpu_amd.power import PowerSampler
+    if args.no_power:
+        return PowerSampler.disabled("--no-power")
+    try:
+        bus = torch.cuda.get_device_properties(local).pci_bus_id
+    except Exception:                                  # noqa: BLE001
+        bus = None
+    return PowerSampler(bus)
+
+
 def init_gloo(dist, rank: int, world: int):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     # gloo's C++ connect messages go to fd 1; keep stdout for the one JSON line (rank 0)
@@ -179,10 +191,15 @@ def main():
                          "eight work items (4096 at k=1, 16384 at k=4), as the CLI's auto batch does "
                          "(engine.cpp batch_chunks)")
     ap.add_argument("--k", type=int, default=1)
-    ap.add_argument("--cpu-seconds", type=float, default=30.0,
-                    help="CPU-baseline window after the table build (a bounded sample: 30 s keeps the default "
-                         "run within a few minutes; the rate is flat from 20 s on, DESIGN.md section 6)")
+    ap.add_argument("--cpu-seconds", type=float, default=60.0,
+                    help="CPU-baseline window after the table build (SURVEY.md section 8d: 60 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-windows", type=int, default=1,
+                    help="repeat the CPU-baseline window this many times and report the mean and spread")
+    ap.add_argument("--no-power", action="store_true", help="do not sample board power during the timed region")
+    ap.add_argument("--share-gpus", action="store_true",
+                    help="allow more ranks than visible GPUs (a multi-rank rehearsal: ranks share GPUs round-robin "
+                         "and the line says so in config.physical_gpus / gpus_shared); refused otherwise")
     ap.add_argument("--no-gate", action="store_true",
                     help="no level-0 gate: every giant step probes the level-1 bloom (the reference's exact candidate "
                          "stream, ~1e-6 false positives per step); not the headline configuration")
@@ -210,11 +227,17 @@ def main():
     import torch                                   # first: share torch's HIP runtime with our libraries
     import torch.distributed as dist
     ndev = torch.cuda.device_count()
+    shared = bool(ndev) and world > ndev
     if ndev and local >= ndev:
+        if not args.share_gpus:
+            # a line from ranks sharing GPUs would read as an N-GPU measurement: refuse
+            raise SystemExit(f"[bench] rank {rank}: LOCAL_RANK {local} >= {ndev} visible GPUs; pass --share-gpus for a "
+                             f"multi-rank rehearsal on fewer GPUs")
         # more ranks than visible GPUs (a multi-rank rehearsal on a smaller box): share round-robin
         print(f"[bench] rank {rank}: LOCAL_RANK {local} >= {ndev} visible GPUs, using GPU {local % ndev}",
               file=sys.stderr, flush=True)
         local = local % ndev
+    gpu_info = {"physical_gpus": min(world, ndev) if ndev else world, "gpus_shared": shared}
     torch.cuda.set_device(local)
     if world > 1:
         init_gloo(dist, rank, world)
@@ -293,17 +316,22 @@ def main():
     if args.warmup:
         sess.run([target], start, end, max_chunks=args.warmup * args.chunks)
     tstart = start + args.warmup * args.chunks * two_n
+    sampler = power_sampler(torch, local, args)
     if world > 1:
         dist.barrier()
     sync()
-    t0 = time.perf_counter()
-    res, st = sess.run([target], tstart, end, max_chunks=args.steps * args.chunks)
-    sync()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+    with sampler:
+        t0 = time.perf_counter()
+        res, st = sess.run([target], tstart, end, max_chunks=args.steps * args.chunks)
+        sync()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
     sess.close()
     steps_done = st["giant_steps"]               # counted on the device (khb_collect, count_walked)
+    psum = sampler.summary(work_units=steps_done, seconds=dt)
+    lanes = khbsgs.default_lanes(local)
+    waves = lanes // (torch.cuda.get_device_properties(local).multi_processor_count * 4 * 64)
     per_launch_steps = args.chunks * tables.cycles * 1024
     kernel_ms = 1e3 * st["kernel_s"] / max(1, st["launches"])
     # device-busy time per step: the union of this rank's launch intervals (HIP events on each launch's
@@ -381,14 +409,23 @@ def main():
         try:
             with open(pmc_path) as f:
                 pmc = json.load(f)
-            if pmc.get("k") == args.k:
+            # the PMC record applies only to the kernel it was measured on
+            run_cfg = {"k": args.k, "level0_gate": not args.no_gate, "lanes": lanes, "waves_per_simd": waves}
+            mism = {key: (pmc.get(key), v) for key, v in run_cfg.items() if pmc.get(key) != v}
+            if mism:
+                roofline["traffic_note"] = ("profiles/pmc_latest.json was measured for another configuration "
+                                            "(%s); traffic not measured for this run" %
+                                            ", ".join("%s %s vs %s" % (k_, a, b) for k_, (a, b) in mism.items()))
+            else:
                 roofline.update(pmc_traffic(pmc, args.chunks, per_launch_steps))
                 roofline["traffic_source"] = os.path.relpath(pmc_path, REPO)
                 if pmc.get("valu_instr_per_giant_step"):
                     vi = pmc["valu_instr_per_giant_step"]
                     executed_info.update({
                         "valu_lane_instr_per_giant_step": vi,
-                        "valu_busy_pct": pmc.get("valu_busy_pct"),
+                        "valu_busy_pct": pmc.get("valu_util_pct"),
+                        "valu_busy_basis": pmc.get("valu_util_basis"),
+                        "valu_busy_4cycle_model_pct": pmc.get("valu_busy_pct"),
                         "valu_lane_instr_T_per_s": round(vi * per_launch_steps / (bmax * 1e-3) / 1e12, 2),
                         "vop3_issue_ceiling": "58-61 lane-instr/clk/CU = %.1f-%.1f T at 2.4 GHz (intops2)"
                                               % (58 * CUS * 2.4e-3, 61 * CUS * 2.4e-3),
@@ -396,6 +433,7 @@ def main():
         except (OSError, ValueError):
             pass
     roofline["executed"] = executed_info
+    roofline["power"] = psum
     # Two launches overlap (the context's two submission slots): a launch's event time
     # includes the tail it shares with its neighbour (kernel_ms_avg > ms_per_step), so `achieved` /
     # `frac` use the device-busy time per step; the per-launch and wall figures are beside them.
@@ -406,11 +444,15 @@ def main():
         c_threads, hinfo = host_cores()
         from oracle import ora                     # the checker-side restatement, timed only here
         cpu_pt = ora.pubkey(PUZZLE66_KEY) if args.workload == "p66" else ora.parse_pubkey(line)[0]
-        v = cpu_baseline(args.cpu_seconds, c_threads, cpu_pt, cpu_base)
+        vs = [cpu_baseline(args.cpu_seconds, c_threads, cpu_pt, cpu_base + w * (1 << 56))
+              for w in range(max(1, args.cpu_windows))]
+        v = sum(vs) / len(vs)
         cpu = {"value": round(v / 1e6, 4), "unit": "Mkeys/s", "cores": c_threads, "kind": "port",
                "sample": f"oracle thread_process_bsgs restatement (k=1, default -n), same target, chunks from "
-                         f"{hex(cpu_base)}, {args.cpu_seconds:.0f} s window on {c_threads} threads (every core this job "
-                         f"may use: host below) after the table build",
+                         f"{hex(cpu_base)}, {len(vs)} x {args.cpu_seconds:.0f} s window(s) on {c_threads} threads "
+                         f"(every core this job may use: host below) after the table build",
+               "window_s": args.cpu_seconds, "windows_mkeys": [round(x / 1e6, 3) for x in vs],
+               "spread_pct": round(100.0 * (max(vs) - min(vs)) / v, 2) if len(vs) > 1 else None,
                "host": hinfo,
                "reference_published": {"value": BSGSD_CPU_MKEYS, "unit": "M giant-steps/s",
                                        "source": "BSGSD.md:52-58 (bsgsd -k 4096 -t 8, unnamed 64 GB server)"}}
@@ -431,6 +473,7 @@ def main():
                    "n": hex(tables.n_low), "bsgs_m": tables.m, "groups_per_chunk": tables.cycles,
                    "chunks_per_step": args.chunks, "giant_steps_per_step": per_launch_steps,
                    "parallelism": "range-partition x%d" % world, "table_build_s": round(t_build, 2),
+                   **gpu_info,
                    "rank0_range": [hex(start), hex(end)],
                    "rank_ranges": [[hex(a), hex(b)] for a, b in ranges],
                    "timed_ranges": [[hex(a + args.warmup * args.chunks * two_n),

@@ -69,12 +69,16 @@ typedef struct {
                               caller rescans the submission in parts -- SURVEY.md §8b) */
   uint32_t n_degenerate;
   uint64_t giant_steps;    /* giant steps the device walked (counted on the device: groups x 1024) */
-  float kernel_ms;         /* device time of the scan kernel (HIP events on the submission's stream) */
+  float kernel_ms;         /* the scan kernel's execution span: from its first workgroup's start to its last
+                              wave's exit on the device's 100 MHz clock (s_memrealtime; khb_submit /
+                              khb_addr_submit), capped by the submission's HIP events, which also count the
+                              time a queued launch waits for CUs behind the other slot's launch */
   double launch_begin_ms;  /* the launch's begin and end on the context's clock: ms since the last
-                              khb_reset_epoch (or khb_open); -1 if unavailable.  Two submissions in flight */
+                              khb_reset_epoch (or khb_open); end = the submission's end event, begin = end -
+                              kernel_ms; -1 if unavailable.  Two submissions in flight */
   double launch_end_ms;    /* overlap, so the union of these intervals is the device-busy time. */
-  float shader_mhz;        /* average shader clock over the launch (s_memtime / s_memrealtime of its first
-                              wave), 0 if unavailable */
+  float shader_mhz;        /* average shader clock over the launch (s_memtime / s_memrealtime from its first
+                              wave's start to its last wave's exit), 0 if unavailable */
 } khb_stats;
 
 /* ---- device / context ---- */

@@ -278,7 +278,9 @@ int confirm_device(Shared& S, khb_ctx* ctx, const Batch& b, const std::vector<kh
 
 // Confirm level-1 candidates (bsgs_secondcheck, keyhunt.cpp:3947-3982): speculative parallel
 // checks (the CPU pool, or the device: SearchConfig::check_mode), then in-order resolution.
-int confirm(Shared& S, khb_ctx* ctx, const Batch& b, std::vector<khb_cand>& cands, int threads) {
+// A failed device check is confirmed on the host pool instead (the same keys); `device_off` then stays
+// set for the calling device thread, which warns once and confirms every later batch on the host.
+void confirm(Shared& S, khb_ctx* ctx, const Batch& b, std::vector<khb_cand>& cands, int threads, bool& device_off) {
   std::sort(cands.begin(), cands.end(), [](const khb_cand& x, const khb_cand& y) {
     return x.job != y.job ? x.job < y.job : x.a < y.a;
   });
@@ -289,13 +291,16 @@ int confirm(Shared& S, khb_ctx* ctx, const Batch& b, std::vector<khb_cand>& cand
     std::lock_guard<std::mutex> lk(S.mu);
     found_snapshot = S.found;
   }
-  bool dev = S.cfg.check_mode == kCheckDevice || (S.cfg.check_mode == kCheckAuto && cands.size() > kCheckAutoMin);
+  bool dev = !device_off &&
+             (S.cfg.check_mode == kCheckDevice || (S.cfg.check_mode == kCheckAuto && cands.size() > kCheckAutoMin));
   if (dev) {
     const int rc = confirm_device(S, ctx, b, cands, found_snapshot, ok, key);
-    if (rc) {      // the host pool confirms this batch instead (the same keys); the search goes on
+    if (rc) {      // the host pool confirms this batch and every later one of this device (the same keys)
+      device_off = true;
       std::lock_guard<std::mutex> lk(S.mu);
       if (S.cb.on_warning)
-        S.cb.on_warning(std::string("[W] device check failed (") + khb_strerror(rc) + "): this batch is confirmed on the host");
+        S.cb.on_warning(std::string("[W] device check failed (") + khb_strerror(rc) +
+                        "): candidates of this device are confirmed on the host from now on");
       std::fill(ok.begin(), ok.end(), 0);
       dev = false;
     }
@@ -319,7 +324,6 @@ int confirm(Shared& S, khb_ctx* ctx, const Batch& b, std::vector<khb_cand>& cand
     if (S.cb.on_found) S.cb.on_found((int)k, key[i]);
   }
   if (S.n_found == (int)S.targets.size()) S.stop = true;   // "All points were found"
-  return KHB_OK;
 }
 
 uint32_t batch_chunks(const Tables& T, const SearchConfig& cfg, size_t ntargets, uint32_t ctx_lanes) {
@@ -409,6 +413,7 @@ void device_thread(Shared& S, khb_ctx* ctx) {
   fill();
   int pre = -1;               // claimed and centred, not yet submitted
   std::vector<khb_cand> cands;
+  bool device_check_off = false;       // a failed khb_check moves this device's confirmations to the host
   while (!q.empty()) {
     if (pre < 0 && !rc && prepare(ring[next])) pre = take();   // overlaps the GPU scan
     const int i = q.front();
@@ -463,8 +468,7 @@ void device_thread(Shared& S, khb_ctx* ctx) {
     }
     if (!overflow) {
       cands.assign(cbuf.begin(), cbuf.begin() + st.n_cand);
-      const int vrc = confirm(S, ctx, b, cands, threads);      // overlaps the GPU scan of the queue
-      if (vrc) { fail(vrc, "khb_check"); rc = vrc; continue; }
+      confirm(S, ctx, b, cands, threads, device_check_off);    // overlaps the GPU scan of the queue
     }
     if (q.empty()) fill();     // rescan parts left after the last batch
   }

@@ -270,7 +270,12 @@ int main(int argc, char** argv) {
         }
         break;
       case 1006: cfg.use_gate = false; break;       // the reference's exact level-1 candidate stream
-      case 'C': case 'E': case 'N': case 'p': case 'v': case 'G': case '8': case 'z':
+      case 'z':                                     // keyhunt.cpp:766-772 (used by initBloomFilter, 6559-6576)
+        ao.bloom_multiplier = (int)strtol(optarg, nullptr, 10);
+        if (ao.bloom_multiplier <= 0) ao.bloom_multiplier = 1;
+        printf("[+] Bloom Size Multiplier %i\n", ao.bloom_multiplier);
+        break;
+      case 'C': case 'E': case 'N': case 'p': case 'v': case 'G': case '8':
         break;   // options of the other search modes
       default:
         fprintf(stderr, "[E] Unknow opcion -%c\n", c);

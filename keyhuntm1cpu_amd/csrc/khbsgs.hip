@@ -104,19 +104,27 @@ __global__ void k_probe(const uint8_t* __restrict__ bloom, BloomGeom g, const Fe
 // One submission's device state.  A context owns two (KHB_QUEUE_DEPTH): khb_submit fills the next
 // free slot on its own stream, so a second batch's workgroups take the CUs the first batch's last
 // waves leave idle (its launch tail), and khb_collect retires the slots in submission order.
+//
+// Round 5: the scans' host hand-over lives in pinned, coherent host memory that the kernel reads and writes in
+// place: the centres (read once per work item), the candidate / degenerate / -m address hit rings (written as
+// hits occur, a few per launch) and a copy of the counters that the launch's last wave writes
+// (launch_epilogue).  A khb_submit stream is then [event, kernel, event] with no memset or copy kernels, and
+// khb_collect only waits for the slot's end event and copies from host memory.
 struct Slot {
   hipStream_t stream = nullptr;
   Fe* d_scratch = nullptr;             // lane-private prefix scratch (allocated on the slot's first use)
-  AffPt* d_centres = nullptr;
-  AffPt* h_centres = nullptr;          // pinned staging
+  AffPt* d_centres = nullptr;          // device copy for the synchronous helpers (dump, baby build)
+  AffPt* h_centres = nullptr;          // pinned, coherent; the scans read it in place
   uint32_t centres_cap = 0;
-  khb_cand* d_cand = nullptr;
-  khb_degenerate* d_degen = nullptr;
-  uint32_t* d_ahits = nullptr;         // -m address hits
+  khb_cand* h_cand = nullptr;          // pinned, coherent rings written by the kernel
+  khb_degenerate* h_degen = nullptr;
+  uint32_t* h_ahits = nullptr;         // -m address hits (allocated on the first -m address submission)
   uint32_t* d_counters = nullptr;
-  uint32_t* h_counters = nullptr;      // pinned
+  uint32_t* h_counters = nullptr;      // pinned, coherent (launch_epilogue, or a copy after the helpers)
+  bool counters_zero = false;          // d_counters is all zero (a scan's epilogue left it so): no memset
   hipEvent_t ev0 = nullptr, ev1 = nullptr;   // launch begin / end (khb_stats: kernel_ms, launch_*_ms)
   uint64_t pending_steps = 0;
+  uint32_t total_waves = 0;            // of the launch in flight (host_counters_ok)
   int kind = 0;                        // in flight: 1 = -m bsgs scan, 2 = -m address scan
 };
 constexpr int kQueueDepth = 2;
@@ -165,6 +173,9 @@ struct khb_ctx {
   CheckOut* d_ck_out = nullptr;
   khb::CPt* d_ck_targets = nullptr;
   uint32_t ck_cap = 0, ck_tcap = 0;
+  // the targets on the device (d_ck_targets) as the caller passed them: a khb_check with the same bytes
+  // uploads only its CheckIn records (no O(n_targets) conversion and upload per batch)
+  std::vector<uint8_t> ck_targets_be;
 };
 
 namespace {
@@ -214,10 +225,15 @@ void free_slot(Slot& S);
 int ensure_slot_alloc(khb_ctx* c, Slot& S) {
   KHB_TRY(c, hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
   KHB_TRY(c, hipMalloc(&S.d_scratch, sizeof(Fe) * kScratchEntries * c->lanes));
-  KHB_TRY(c, hipMalloc(&S.d_cand, sizeof(khb_cand) * kCandCap));
-  KHB_TRY(c, hipMalloc(&S.d_degen, sizeof(khb_degenerate) * kDegenCap));
+  KHB_TRY(c, hipHostMalloc((void**)&S.h_cand, sizeof(khb_cand) * kCandCap, hipHostMallocCoherent));
+  KHB_TRY(c, hipHostMalloc((void**)&S.h_degen, sizeof(khb_degenerate) * kDegenCap, hipHostMallocCoherent));
   KHB_TRY(c, hipMalloc(&S.d_counters, kCounterBytes));
-  KHB_TRY(c, hipHostMalloc((void**)&S.h_counters, kCounterBytes, hipHostMallocDefault));
+  // on the slot's own stream: a null-stream hipMemset of device memory may still be queued (behind the other
+  // slot's running launch, for CU slots) when this slot's first launch starts, and would zero its counters
+  // mid-launch (round 5: a lazily allocated slot 1 re-walked 6,144 groups, tools/debug/epilogue_diag.py)
+  KHB_TRY(c, hipMemsetAsync(S.d_counters, 0, kCounterBytes, S.stream));
+  S.counters_zero = true;
+  KHB_TRY(c, hipHostMalloc((void**)&S.h_counters, kHostCounterBytes, hipHostMallocCoherent));
   KHB_TRY(c, hipEventCreate(&S.ev0));
   KHB_TRY(c, hipEventCreate(&S.ev1));
   return KHB_OK;
@@ -234,9 +250,9 @@ void free_slot(Slot& S) {
   if (S.stream) hipStreamSynchronize(S.stream);
   hipFree(S.d_scratch);
   hipFree(S.d_centres);
-  hipFree(S.d_cand);
-  hipFree(S.d_degen);
-  hipFree(S.d_ahits);
+  if (S.h_cand) hipHostFree(S.h_cand);
+  if (S.h_degen) hipHostFree(S.h_degen);
+  if (S.h_ahits) hipHostFree(S.h_ahits);
   hipFree(S.d_counters);
   if (S.h_counters) hipHostFree(S.h_counters);
   if (S.h_centres) hipHostFree(S.h_centres);
@@ -255,7 +271,7 @@ int ensure_centres(khb_ctx* c, Slot& S, uint32_t n) {
   S.centres_cap = 0;
   uint32_t cap = n < 1024 ? 1024 : n;
   KHB_TRY(c, hipMalloc(&S.d_centres, sizeof(AffPt) * cap));
-  KHB_TRY(c, hipHostMalloc((void**)&S.h_centres, sizeof(AffPt) * cap, hipHostMallocDefault));
+  KHB_TRY(c, hipHostMalloc((void**)&S.h_centres, sizeof(AffPt) * cap, hipHostMallocCoherent));
   S.centres_cap = cap;
   return KHB_OK;
 }
@@ -289,8 +305,8 @@ ScanArgs make_args(khb_ctx* c, const Slot& S, uint32_t n_jobs, uint32_t group_be
   A.gofs = c->gpl == 1 ? c->d_offs : c->d_gofs;
   A.centres = S.d_centres;
   A.scratch = S.d_scratch;
-  A.cand = S.d_cand;
-  A.degen = S.d_degen;
+  A.cand = S.h_cand;
+  A.degen = S.h_degen;
   A.counters = S.d_counters;
   A.n_jobs = n_jobs;
   A.group_begin = group_begin;
@@ -307,24 +323,40 @@ ScanArgs make_args(khb_ctx* c, const Slot& S, uint32_t n_jobs, uint32_t group_be
 // kernel_ms and the launch's interval on the context's clock (khb_reset_epoch), from the slot's events;
 // the shader clock from the kernel's clock_probe samples.
 // Called after S's stream has drained (the slot's launch is complete and the stream idle).
+//
+// Round 5: a scan launched by khb_submit / khb_addr_submit (launch_epilogue) is timed by its own clocks: block 0's
+// first wave samples s_memtime / s_memrealtime when it starts (the launch's first workgroup) and the launch's last
+// wave when it leaves, so kernel_ms is the launch's execution span on the 100 MHz clock and the shader clock is
+// the average over that span.  The interval on the context's clock ends at the slot's end event and begins that
+// span earlier.  The events alone would also count the time the queued launch waits, dispatched, for the CUs
+// the other slot's running launch still holds (nothing but a kernel sits on the slot's stream since round 5).
 constexpr float kReanchorMs = 60000.f;
-void launch_times(khb_ctx* c, const Slot& S, khb_stats* st) {
-  uint64_t p[4];
+void launch_times(khb_ctx* c, const Slot& S, khb_stats* st, bool epilogue) {
+  uint64_t p[4], q[2];
   memcpy(p, S.h_counters + 8, sizeof p);
-  st->shader_mhz = (p[3] > p[1] && p[2] > p[0]) ? (float)(100.0 * (double)(p[2] - p[0]) / (double)(p[3] - p[1])) : 0.f;
+  memcpy(q, S.h_counters + 16, sizeof q);
+  // The shader clock from block 0's first wave alone (its start and exit): s_memtime counts per XCD, so a
+  // ratio across two waves on different XCDs is meaningless.  The 100 MHz s_memrealtime is one clock for the
+  // whole device: the execution span runs from block 0's start to the last wave's exit (q[1]).
+  const bool clocks = p[3] > p[1] && p[2] > p[0];
+  st->shader_mhz = clocks ? (float)(100.0 * (double)(p[2] - p[0]) / (double)(p[3] - p[1])) : 0.f;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, S.ev0, S.ev1) != hipSuccess) ms = -1.f;
+  if (epilogue && q[1] > p[1] && ms >= 0.f) {
+    const float span = (float)((double)(q[1] - p[1]) * 1e-5);     // 100 MHz ticks -> ms
+    if (span < ms) ms = span;
+  }
   st->kernel_ms = ms;
-  float b = -1.f, bp = -1.f;
-  double begin = -1.0;
+  float e = -1.f, ep = -1.f, b = -1.f;
+  double end = -1.0;
   const bool cur = c->epoch && hipEventElapsedTime(&b, c->epoch, S.ev0) == hipSuccess && b >= 0.f;
-  if (cur)
-    begin = c->epoch_ms + (double)b;
-  else if (c->have_prev && hipEventElapsedTime(&bp, c->epoch_prev, S.ev0) == hipSuccess && bp >= 0.f)
-    begin = c->epoch_prev_ms + (double)bp;
-  if (begin >= 0.0 && ms >= 0.f) {
-    st->launch_begin_ms = begin;
-    st->launch_end_ms = begin + (double)ms;
+  if (cur && hipEventElapsedTime(&e, c->epoch, S.ev1) == hipSuccess && e >= 0.f)
+    end = c->epoch_ms + (double)e;
+  else if (c->have_prev && hipEventElapsedTime(&ep, c->epoch_prev, S.ev1) == hipSuccess && ep >= 0.f)
+    end = c->epoch_prev_ms + (double)ep;
+  if (end >= 0.0 && ms >= 0.f) {
+    st->launch_begin_ms = end - (double)ms;
+    st->launch_end_ms = end;
   } else {
     st->launch_begin_ms = st->launch_end_ms = -1.0;
   }
@@ -339,6 +371,23 @@ void launch_times(khb_ctx* c, const Slot& S, khb_stats* st) {
     c->have_prev = true;
   }
 }
+
+// The scans' launch without copy kernels: centres read in place from the slot's pinned block, counters
+// zeroed by the previous scan's epilogue (a memset only after a helper used them), the last wave's copy of
+// them in h_counters; h_counters[3] is poisoned so that khb_collect can tell the epilogue ran.
+int prepare_host_launch(khb_ctx* c, Slot& S, ScanArgs& A, uint32_t blocks) {
+  if (!S.counters_zero) KHB_TRY(c, hipMemsetAsync(S.d_counters, 0, kCounterBytes, S.stream));
+  S.counters_zero = false;             // until khb_collect sees the epilogue's copy
+  memset(S.h_counters, 0, kHostCounterBytes);
+  S.h_counters[3] = 0xFFFFFFFFu;
+  A.centres = S.h_centres;
+  A.host_counters = S.h_counters;
+  A.total_waves = blocks * kWavesPerBlock;
+  return KHB_OK;
+}
+
+// After the slot's end event: the epilogue's copy is complete iff it counted every wave of the launch.
+bool host_counters_ok(const Slot& S, uint32_t total_waves) { return S.h_counters[3] == total_waves; }
 
 int check_scan_args(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count,
                     bool bsgs = true) {
@@ -606,14 +655,13 @@ int khb_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t gro
   ScanArgs A = make_args(c, S, n_jobs, group_begin, group_count, kBatch);
   if (A.n_items > 0xFFFFFF00ull) return KHB_EINVAL;      // the 32-bit work-item counter (KHB_DYN)
   pts_from_be(S.h_centres, centres, n_jobs);
-  KHB_TRY(c, hipMemcpyAsync(S.d_centres, S.h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, S.stream));
-  KHB_TRY(c, hipMemsetAsync(S.d_counters, 0, kCounterBytes, S.stream));
   const uint32_t blocks = c->lanes / kBlock;
+  if ((rc = prepare_host_launch(c, S, A, blocks))) return rc;
   KHB_TRY(c, hipEventRecord(S.ev0, S.stream));
   launch_bsgs(c->d_gate1 ? kScanG1 : c->d_gate ? kScanG : kScan, blocks, S.stream, A);
   KHB_TRY(c, hipGetLastError());
   KHB_TRY(c, hipEventRecord(S.ev1, S.stream));
-  KHB_TRY(c, hipMemcpyAsync(S.h_counters, S.d_counters, kCounterBytes, hipMemcpyDeviceToHost, S.stream));
+  S.total_waves = A.total_waves;
   S.kind = 1;
   S.pending_steps = (uint64_t)n_jobs * group_count * KHB_GROUP;
   c->queued++;
@@ -628,20 +676,22 @@ int khb_collect(khb_ctx* c, khb_cand* cand, uint32_t cap, khb_degenerate* degen,
   S.kind = 0;
   c->head = (c->head + 1) % kQueueDepth;
   c->queued--;
-  KHB_TRY(c, hipStreamSynchronize(S.stream));
+  KHB_TRY(c, hipEventSynchronize(S.ev1));
+  if (!host_counters_ok(S, S.total_waves)) return KHB_EHIP;   // the launch's epilogue did not complete
+  S.counters_zero = true;
   const uint32_t nc = S.h_counters[0], nd = S.h_counters[1];
   uint32_t take = nc < c->cand_cap ? nc : c->cand_cap;
   if (take > cap) take = cap;
-  if (take && cand) KHB_TRY(c, hipMemcpy(cand, S.d_cand, sizeof(khb_cand) * take, hipMemcpyDeviceToHost));
+  if (take && cand) memcpy(cand, S.h_cand, sizeof(khb_cand) * take);
   uint32_t dt = nd < kDegenCap ? nd : kDegenCap;
   if (dt > degen_cap) dt = degen_cap;
-  if (dt && degen) KHB_TRY(c, hipMemcpy(degen, S.d_degen, sizeof(khb_degenerate) * dt, hipMemcpyDeviceToHost));
+  if (dt && degen) memcpy(degen, S.h_degen, sizeof(khb_degenerate) * dt);
   const uint64_t steps = walked_groups(S) * KHB_GROUP;
   if (st) {
     st->n_cand = nc;
     st->n_degenerate = nd;
     st->giant_steps = steps;
-    launch_times(c, S, st);
+    launch_times(c, S, st, true);
   }
   return steps == S.pending_steps ? KHB_OK : KHB_EINCOMPLETE;
 }
@@ -668,6 +718,7 @@ int khb_dump_x(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint32_t
   KHB_TRY(c, hipMalloc(&d_x, bytes));
   hipError_t e = hipMemcpyAsync(S.d_centres, S.h_centres, sizeof(AffPt), hipMemcpyHostToDevice, S.stream);
   if (e == hipSuccess) e = hipMemsetAsync(S.d_counters, 0, kCounterBytes, S.stream);
+  S.counters_zero = false;
   if (e == hipSuccess) {
     ScanArgs A = make_args(c, S, 1, group_begin, group_count, kBatch);
     A.xdump = d_x;
@@ -761,21 +812,21 @@ int khb_addr_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_
   if (!Sp) return rc;
   Slot& S = *Sp;
   if ((rc = ensure_centres(c, S, n_jobs))) return rc;
-  if (!S.d_ahits) KHB_TRY(c, hipMalloc(&S.d_ahits, sizeof(khb_addr_hit) * kAddrHitCap));
+  if (!S.h_ahits)
+    KHB_TRY(c, hipHostMalloc((void**)&S.h_ahits, sizeof(khb_addr_hit) * kAddrHitCap, hipHostMallocCoherent));
   pts_from_be(S.h_centres, centres, n_jobs);
-  KHB_TRY(c, hipMemcpyAsync(S.d_centres, S.h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, S.stream));
-  KHB_TRY(c, hipMemsetAsync(S.d_counters, 0, kCounterBytes, S.stream));
   ScanArgs A = make_args(c, S, n_jobs, group_begin, group_count);
   A.bloom = c->d_abloom;
   A.geom = c->ageom;
-  A.ahits = S.d_ahits;
+  A.ahits = S.h_ahits;
   A.ahit_cap = khb_addr_hit_capacity(c);
   const uint32_t blocks = c->lanes / kBlock;
+  if ((rc = prepare_host_launch(c, S, A, blocks))) return rc;
   KHB_TRY(c, hipEventRecord(S.ev0, S.stream));
   launch_addr(search == 0 ? kAddrU : search == 1 ? kAddrC : kAddrB, blocks, S.stream, A);
   KHB_TRY(c, hipGetLastError());
   KHB_TRY(c, hipEventRecord(S.ev1, S.stream));
-  KHB_TRY(c, hipMemcpyAsync(S.h_counters, S.d_counters, kCounterBytes, hipMemcpyDeviceToHost, S.stream));
+  S.total_waves = A.total_waves;
   S.kind = 2;
   S.pending_steps = (uint64_t)n_jobs * group_count * KHB_GROUP;
   c->queued++;
@@ -790,18 +841,20 @@ int khb_addr_collect(khb_ctx* c, khb_addr_hit* hits, uint32_t cap, khb_stats* st
   S.kind = 0;
   c->head = (c->head + 1) % kQueueDepth;
   c->queued--;
-  KHB_TRY(c, hipStreamSynchronize(S.stream));
+  KHB_TRY(c, hipEventSynchronize(S.ev1));
+  if (!host_counters_ok(S, S.total_waves)) return KHB_EHIP;   // the launch's epilogue did not complete
+  S.counters_zero = true;
   const uint32_t nh = S.h_counters[0], nd = S.h_counters[1];
   const uint32_t acap = khb_addr_hit_capacity(c);
   uint32_t take = nh < acap ? nh : acap;
   if (take > cap) take = cap;
-  if (take && hits) KHB_TRY(c, hipMemcpy(hits, S.d_ahits, sizeof(khb_addr_hit) * take, hipMemcpyDeviceToHost));
+  if (take && hits) memcpy(hits, S.h_ahits, sizeof(khb_addr_hit) * take);
   const uint64_t steps = walked_groups(S) * KHB_GROUP;
   if (st) {
     st->n_cand = nh;
     st->n_degenerate = nd;
     st->giant_steps = steps;
-    launch_times(c, S, st);
+    launch_times(c, S, st, true);
   }
   return steps == S.pending_steps ? KHB_OK : KHB_EINCOMPLETE;
 }
@@ -828,6 +881,7 @@ int khb_addr_dump(khb_ctx* c, const uint8_t* centre, uint32_t group_begin, uint3
   KHB_TRY(c, hipMalloc(&d_xy, bytes));
   hipError_t e = hipMemcpyAsync(S.d_centres, S.h_centres, sizeof(AffPt), hipMemcpyHostToDevice, S.stream);
   if (e == hipSuccess) e = hipMemsetAsync(S.d_counters, 0, kCounterBytes, S.stream);
+  S.counters_zero = false;
   if (e == hipSuccess) {
     ScanArgs A = make_args(c, S, 1, group_begin, group_count);
     A.xdump = d_xy;
@@ -905,6 +959,7 @@ int ensure_check_buffers(khb_ctx* c, uint32_t n, uint32_t n_targets) {
     c->ck_cap = cap;
   }
   if (n_targets > c->ck_tcap) {
+    c->ck_targets_be.clear();
     hipFree(c->d_ck_targets);
     c->d_ck_targets = nullptr;
     c->ck_tcap = 0;
@@ -983,16 +1038,23 @@ int khb_check(khb_ctx* c, const uint8_t* targets_xy, uint32_t n_targets, const k
   if (rc) return rc;
   std::vector<CheckIn> hin(n);
   std::vector<CheckOut> hout(n);
-  std::vector<khb::CPt> ht(n_targets);
   for (uint32_t i = 0; i < n; ++i) {
     hin[i].start = u8_from_be(in[i].start_be);
     hin[i].a = in[i].a;
     hin[i].target = in[i].target;
   }
-  cpts_from_be(ht.data(), targets_xy, n_targets);
   KHB_TRY(c, hipMemcpyAsync(c->d_ck_in, hin.data(), sizeof(CheckIn) * n, hipMemcpyHostToDevice, c->ck_stream));
-  KHB_TRY(c, hipMemcpyAsync(c->d_ck_targets, ht.data(), sizeof(khb::CPt) * n_targets, hipMemcpyHostToDevice,
-                            c->ck_stream));
+  const size_t tbytes = 64 * (size_t)n_targets;
+  const bool same = c->ck_targets_be.size() == tbytes && (tbytes == 0 || !memcmp(c->ck_targets_be.data(), targets_xy, tbytes));
+  std::vector<khb::CPt> ht;
+  if (!same) {
+    ht.resize(n_targets);
+    cpts_from_be(ht.data(), targets_xy, n_targets);
+    c->ck_targets_be.clear();            // invalid until the upload below has been issued
+    KHB_TRY(c, hipMemcpyAsync(c->d_ck_targets, ht.data(), sizeof(khb::CPt) * n_targets, hipMemcpyHostToDevice,
+                              c->ck_stream));
+    c->ck_targets_be.assign(targets_xy, targets_xy + tbytes);
+  }
   launch_check(c->ck_stream, c->ck, c->d_ck_in, c->d_ck_targets, n_targets, c->d_ck_out, n);
   KHB_TRY(c, hipGetLastError());
   KHB_TRY(c, hipMemcpyAsync(hout.data(), c->d_ck_out, sizeof(CheckOut) * n, hipMemcpyDeviceToHost, c->ck_stream));
@@ -1062,6 +1124,7 @@ int khb_build_baby(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t
   if (e == hipSuccess)
     e = hipMemcpyAsync(S.d_centres, S.h_centres, sizeof(AffPt) * n_jobs, hipMemcpyHostToDevice, S.stream);
   if (e == hipSuccess) e = hipMemsetAsync(S.d_counters, 0, kCounterBytes, S.stream);
+  S.counters_zero = false;
   if (e == hipSuccess) e = hipEventRecord(S.ev0, S.stream);
   if (e == hipSuccess) {
     launch_baby(c->lanes / kBlock, S.stream, A);

@@ -44,6 +44,11 @@ constexpr uint32_t kBlock = 256;
 #define KHB_BATCH 8               // -m bsgs groups per work item (scan_batch): two inversions per item
 #endif
 constexpr uint32_t kBatch = KHB_BATCH;
+#ifndef KHB_HALF_STREAM
+// 1: the forward pass stores only the odd prefixes P_1, P_3, ..., P_509 and the walk rebuilds each even one
+// from its odd neighbour (one extra product per two walk steps, half the prefix stream)
+#define KHB_HALF_STREAM 0
+#endif
 
 // Kernel modes (template argument of scan_group / k_giant_scan).
 enum : int {
@@ -71,6 +76,7 @@ constexpr uint32_t kCandCap = 1u << 20;
 constexpr uint32_t kAddrHitCap = 1u << 18;
 constexpr uint32_t kDegenCap = 4096;
 constexpr size_t kCounterBytes = 64;                 // ScanArgs::counters
+constexpr size_t kHostCounterBytes = 128;            // ScanArgs::host_counters (launch_epilogue)
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
@@ -96,14 +102,19 @@ struct ScanArgs {
   const AffPt* __restrict__ gsn;       // [0..511] GSn, [512] _2GSn
   const AffPt* __restrict__ offs;      // lane start offsets
   const AffPt* __restrict__ gofs;      // per-group centre offsets j*_2GSn (scan_batch)
-  const AffPt* __restrict__ centres;   // per-job group-0 centre
+  const AffPt* __restrict__ centres;   // per-job group-0 centre (khb_submit: pinned host memory, read in place)
   Fe* __restrict__ scratch;            // prefix products [512][lanes]
-  khb_cand* __restrict__ cand;
-  khb_degenerate* __restrict__ degen;
+  khb_cand* __restrict__ cand;         // candidate ring (khb_submit: pinned host memory, written in place)
+  khb_degenerate* __restrict__ degen;  // degenerate-group ring (same)
   uint32_t* __restrict__ counters;     // [0] candidates [1] degenerate groups [2] work-item cursor (dynamic items)
+                                       // [3] waves finished (launch_epilogue)
                                        // [4..5] groups walked (u64, count_walked)
                                        // [8..15] shader clock probe (clock_probe): memtime, realtime at the
                                        // first wave's start, then at its end (u64 each)
+  uint32_t* __restrict__ host_counters;  // launch_epilogue: the last wave copies counters[0..15] here (pinned host
+                                         // memory), adds its end clocks at [16..19] and zeroes counters[0..7] for
+                                         // the slot's next launch; null = off
+  uint32_t total_waves;                // waves of the launch (launch_epilogue)
   uint8_t* __restrict__ xdump;         // dump modes only
   uint32_t* __restrict__ ahits;        // -m address hits: {job, group, t, kind} x ahit_cap
   uint32_t ahit_cap;
@@ -615,6 +626,84 @@ __device__ __forceinline__ void walk_group_g(const ScanArgs& A, ProbeQueue& Q, c
   probe<false>(A, Q, C.x, job, j, kHalf);        // the centre, pts[512]
 }
 
+// walk_group_g over the half prefix stream (KHB_HALF_STREAM): the forward pass stored only the odd prefixes.
+// After the peeled step 511 the walk goes in pairs (even i, odd i - 1): the even step needs P_{i-1}, stored,
+// and then loads P_{i-3}; the odd step rebuilds P_{i-2} = P_{i-3} * dx_{i-2} (one extra product per pair).
+// Same points, same order and bit-identical x: P_{i-2} is the forward pass's own product of the same
+// operands in the same order.
+template <bool STAGE1>
+__device__ __forceinline__ void half_points(const ScanArgs& A, ProbeQueue& Q, const AffPt& C, const Fe& negCx,
+                                            const Fe& negCy, const Fe& idx, int i, uint32_t base, uint32_t job) {
+  const GsnTable gsn{A.gsn};
+  Fe u, s, x1, x2;
+  const AffPt g = gsn.pt(i);
+  fm_add_lazy(u, gsn.nx(i), negCx);             // nu = -(C.x + GSn.x)
+  fm_add_lazy(s, g.y, C.y);
+  fm_mul(s, s, idx);
+  fm_sqr_add(x1, s, u);
+  x_out<kScanG>(A, x1);
+  fm_add_lazy(s, g.y, negCy);
+  fm_mul(s, s, idx);
+  fm_sqr_add(x2, s, u);
+  x_out<kScanG>(A, x2);
+  gate_pair<STAGE1>(A, Q, x1, base + kHalf - 1 - (uint32_t)i, true, x2, base + kHalf + 1 + (uint32_t)i, job);
+}
+
+template <bool STAGE1>
+__device__ __forceinline__ void walk_group_g_half(const ScanArgs& A, ProbeQueue& Q, const AffPt& C, Fe inv,
+                                                  uint32_t job, uint32_t j, const Fe* scr) {
+  const size_t S = A.stride;
+  const GsnTable gsn{A.gsn};
+  const uint32_t base = j * KHB_GROUP;
+  Fe negCx, negCy;
+  {
+    Fe p;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p.v[k] = k == 0 ? KHB_P0 : (k == 1 ? KHB_P1 : 0xFFFFFFFFu);
+    fm_sub(negCx, p, C.x);
+    fm_sub(negCy, p, C.y);
+  }
+  Fe pre = scr_ld(scr + (size_t)(kHalf - 3) * S);          // P_509
+  Fe idx, dx;
+  // odd step 511: pts[0] = C - GSn[511] only
+  {
+    Fe u, s, x1;
+    fm_add_lazy(dx, gsn.x(kHalf - 2), negCx);
+    fm_mul(idx, pre, dx);                                  // P_510 = P_509 * dx_510
+    fm_mul(idx, inv, idx);
+    fm_add_lazy(dx, gsn.x(kHalf - 1), negCx);
+    fm_mul(inv, inv, dx);
+    const AffPt g = gsn.pt(kHalf - 1);
+    fm_add_lazy(u, gsn.nx(kHalf - 1), negCx);
+    fm_add_lazy(s, g.y, C.y);
+    fm_mul(s, s, idx);
+    fm_sqr_add(x1, s, u);
+    x_out<kScanG>(A, x1);
+    gate_pair<STAGE1>(A, Q, x1, base, false, x1, 0, job);
+  }
+  // pairs (even i, odd i - 1), i = 510 ... 2; pre = P_{i-1} on entry
+  for (int i = (int)kHalf - 2; i >= 2; i -= 2) {
+    fm_mul(idx, inv, pre);                                 // even step i: P_{i-1} (odd index, stored)
+    if (i > 2) pre = scr_ld(scr + (size_t)(i - 3) * S);    // P_{i-3} for step i - 1 (and i - 2)
+    fm_add_lazy(dx, gsn.x(i), negCx);
+    fm_mul(inv, inv, dx);
+    half_points<STAGE1>(A, Q, C, negCx, negCy, idx, i, base, job);
+    // odd step i - 1: P_{i-2} = P_{i-3} * dx_{i-2} (i - 1 = 1: P_0 = dx_0)
+    fm_add_lazy(dx, gsn.x(i - 2), negCx);
+    if (i > 2) {
+      fm_mul(idx, pre, dx);
+      fm_mul(idx, inv, idx);
+    } else {
+      fm_mul(idx, inv, dx);
+    }
+    fm_add_lazy(dx, gsn.x(i - 1), negCx);
+    fm_mul(inv, inv, dx);
+    half_points<STAGE1>(A, Q, C, negCx, negCy, idx, i - 1, base, job);
+  }
+  half_points<STAGE1>(A, Q, C, negCx, negCy, inv, 0, base, job);     // step 0: idx = inv
+  probe<false>(A, Q, C.x, job, j, kHalf);
+}
+
 // One reference group centred on C, walked on its own (-m address, baby steps): the 513-element
 // batch of IntGroup.cpp:36-58 including dx[512] = _2GSn.x - C.x, whose inverse advances C to the
 // next centre (keyhunt.cpp:3986-3999).  For -m address this is keyhunt.cpp:2586-2711 with the
@@ -811,11 +900,11 @@ __device__ __forceinline__ uint32_t scan_batch(const ScanArgs& A, ProbeQueue& Q,
     }
     // dx_i = GSn[i].x - C.x as the lazy sum GSn[i].x + (p - C.x) (congruent; feeds products only)
     fm_add_lazy(a, gsn.x(0), negCx);
-    scr_st(sg, a);
+    if (!(is_gated(MODE) && KHB_HALF_STREAM)) scr_st(sg, a);
     for (uint32_t i = 1; i < kHalf - 1; ++i) {
       fm_add_lazy(dx, gsn.x(i), negCx);
       fm_mul(a, a, dx);
-      scr_st(sg + i * S, a);
+      if (!(is_gated(MODE) && KHB_HALF_STREAM) || (i & 1u)) scr_st(sg + i * S, a);
     }
     fm_add_lazy(dx, gsn.x(kHalf - 1), negCx);
     fm_mul(a, a, dx);
@@ -849,7 +938,9 @@ __device__ __forceinline__ uint32_t scan_batch(const ScanArgs& A, ProbeQueue& Q,
     Fe* const sg = scr + (size_t)g * kHalf * S;
     asm volatile("" ::: "memory");
     const AffPt C{sc[2 * g * S], sc[(2 * g + 1) * S]};
-    if constexpr (is_gated(MODE))
+    if constexpr (is_gated(MODE) && KHB_HALF_STREAM)
+      walk_group_g_half<MODE == kScanG1>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
+    else if constexpr (is_gated(MODE))
       walk_group_g<MODE == kScanG1>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
     else
       walk_group<MODE>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
@@ -880,9 +971,40 @@ __device__ __forceinline__ void clock_probe(uint32_t* counters, int at) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const uint64_t t = __builtin_amdgcn_s_memtime(), r = __builtin_amdgcn_s_memrealtime();
     uint64_t* c = reinterpret_cast<uint64_t*>(counters + 8) + 2 * at;
-    c[0] = t;
-    c[1] = r;
+    // agent-scope (write-through) vector stores: launch_epilogue's last wave may run on another XCD
+    __hip_atomic_store(c, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(c + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// End of a launch without copy kernels (round 5): every wave releases its counter updates and adds one to
+// counters[3]; the wave whose add is the launch's last reads the counters memory-side (agent-scope atomics,
+// coherent across the XCDs' L2s), writes them to the slot's pinned host block with vector stores and zeroes
+// counters[0..7] for the slot's next launch.  With the candidate / degenerate rings and the centres in
+// pinned host memory as well, a khb_submit stream holds only this kernel and its two events: no memset
+// before it and no device-to-host blit after it, which had waited for CU slots behind the other slot's
+// persistent scan.  khb_collect checks host counters[3] == total_waves.
+__device__ __forceinline__ void launch_epilogue(const ScanArgs& A) {
+  if (!A.host_counters) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");     // this wave's atomics and probe stores have landed
+  uint32_t prev = 0;
+  if ((threadIdx.x & 63u) == 0)
+    prev = __hip_atomic_fetch_add(&A.counters[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  prev = __shfl(prev, 0);
+  if (prev != A.total_waves - 1) return;
+  const uint32_t l = threadIdx.x & 63u;
+  if (l < 16) {
+    const uint32_t v = l < 8 ? __hip_atomic_exchange(&A.counters[l], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : __hip_atomic_fetch_add(&A.counters[l], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    A.host_counters[l] = v;
+  }
+  // the launch's end on the shader clock and the 100 MHz clock ([16..19]): with block 0's start sample on the
+  // 100 MHz clock ([10..11]; s_memrealtime is one clock for the device, s_memtime one per XCD) the host gets
+  // the launch's execution span, which the events cannot give while the other slot's launch still holds the
+  // CUs the queued kernel waits for (khb_stats.kernel_ms)
+  const uint64_t t = __builtin_amdgcn_s_memtime(), r = __builtin_amdgcn_s_memrealtime();
+  if (l < 4) A.host_counters[16 + l] = (uint32_t)((l < 2 ? t : r) >> (32 * (l & 1u)));
+  __threadfence_system();
 }
 
 template <int MODE>
@@ -946,6 +1068,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(MODE)) void k_giant_scan(Sca
   if (QUEUE) q_drain(A, Q, 1);   // the wave has reconverged: finish what is still queued
   count_walked(A.counters, walked);
   clock_probe(A.counters, 1);
+  launch_epilogue(A);
 }
 
 // Launchers of the k_giant_scan instances (one translation unit each, see above).

@@ -75,10 +75,14 @@ def _kill_group(p: subprocess.Popen, sig: int):
         pass
 
 
-def spawn_ranks(world: int, cmd: Sequence[str], env: Mapping[str, str] | None = None, grace_s: float = 15.0) -> int:
+def spawn_ranks(world: int, cmd: Sequence[str], env: Mapping[str, str] | None = None, grace_s: float = 15.0,
+                straggler_s: float = 300.0, timeout_s: float | None = None) -> int:
     """Run `cmd` as `world` rank processes; rank 0's stdout is forwarded to ours, the other ranks' stdout
     goes to our stderr (stdout keeps exactly rank 0's JSON line).  When a rank fails, the others are
-    terminated (SIGTERM, then SIGKILL after grace_s) and its exit status is returned; 0 when all succeed."""
+    terminated (SIGTERM, then SIGKILL after grace_s) and its exit status is returned; 0 when all succeed.
+    Once any rank has exited, the others have straggler_s to follow (the ranks meet in a final barrier, so a
+    rank still running then is stuck); with timeout_s the whole run has that long.  Either limit stops the
+    remaining ranks the same way and returns 124, as timeout(1) does."""
     base = dict(os.environ if env is None else env)
     port = free_port()
     procs: list[subprocess.Popen] = []
@@ -99,29 +103,47 @@ def spawn_ranks(world: int, cmd: Sequence[str], env: Mapping[str, str] | None = 
             t.start()
             pumps.append(t)
         live = set(range(world))
+        t_start = time.time()
+        first_exit = None
+
+        def stop_live():
+            for q in live:
+                _kill_group(procs[q], signal.SIGTERM)
+            deadline = time.time() + grace_s
+            for q in list(live):
+                try:
+                    procs[q].wait(timeout=max(0.1, deadline - time.time()))
+                except subprocess.TimeoutExpired:
+                    _kill_group(procs[q], signal.SIGKILL)
+                    procs[q].wait()
+            live.clear()
+
         while live:
             for r in sorted(live):
                 c = procs[r].poll()
                 if c is None:
                     continue
                 live.discard(r)
+                if first_exit is None:
+                    first_exit = time.time()
                 if c != 0 and rc == 0:
                     rc = c if c > 0 else 128 - c          # a signal -s reads as 128 + s, like a shell
                     print(f"[bench] rank {r} exited with status {c}; stopping the other ranks",
                           file=sys.stderr, flush=True)
-                    for q in live:
-                        _kill_group(procs[q], signal.SIGTERM)
-                    deadline = time.time() + grace_s
-                    for q in list(live):
-                        try:
-                            procs[q].wait(timeout=max(0.1, deadline - time.time()))
-                        except subprocess.TimeoutExpired:
-                            _kill_group(procs[q], signal.SIGKILL)
-                            procs[q].wait()
-                    live.clear()
+                    stop_live()
                     break
-            if live:
-                time.sleep(0.2)
+            if not live:
+                break
+            now = time.time()
+            late = first_exit is not None and now - first_exit > straggler_s
+            if late or (timeout_s is not None and now - t_start > timeout_s):
+                print(f"[bench] ranks {sorted(live)} still running "
+                      + (f"{straggler_s:.0f} s after another rank exited" if late else f"after {timeout_s:.0f} s")
+                      + "; stopping them", file=sys.stderr, flush=True)
+                stop_live()
+                rc = rc or 124
+                break
+            time.sleep(0.2)
     finally:
         for p in procs:
             if p.poll() is None:

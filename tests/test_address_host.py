@@ -119,3 +119,38 @@ def test_host_generator_matches_oracle(ora, stride):
     assert gpl == 4 and len(offs) // 64 == 16
     for m in (1, 2, 15):
         assert offs[64 * m:64 * m + 64] == ora.pubkey(m * gpl * 1024 * stride).be64()
+
+
+def _many_rmd_lines(n, seed=5):
+    rng = random.Random(seed)
+    return "\n".join("%040x" % rng.getrandbits(160) for _ in range(n)) + "\n"
+
+
+@pytest.mark.parametrize("mult", [1, 4])
+def test_host_bloom_multiplier_matches_oracle(ora, mult):
+    """-z (FLAGBLOOMMULTIPLIER, keyhunt.cpp:766-772): initBloomFilter sizes the target bloom for
+    multiplier x items when the file holds more than 10,000 targets (6559-6576).  12,000 synthetic
+    hash160 lines: the host's bloom is byte-equal to the oracle's at -z 1 and -z 4, and -z 4's is the
+    oracle's bloom_init2(4 x 12,000) geometry (larger than -z 1's)."""
+    text = _many_rmd_lines(12000)
+    A = khhost.Addr(text, n_seq=1 << 16, threads=4, bloom_multiplier=mult)
+    O = ora.AddrTable(text, bloom_multiplier=mult)
+    bf, bits, h = A.bloom()
+    assert bits == O.bloom().bits and h == O.bloom().hashes and bf == O.bloom_bytes()
+    ref = ora.AddrTable(text, bloom_multiplier=1)
+    if mult == 4:
+        assert bits > ref.bloom().bits
+        assert O.bloom().entries == 4 * 12000
+    ref.close()
+    O.close()
+    A.close()
+
+
+def test_host_bloom_multiplier_clamped_below_10000(ora):
+    """At most 10,000 targets: the bloom is sized for 10,000 entries whatever -z says (6561-6566)."""
+    text = _many_rmd_lines(500)
+    a1 = khhost.Addr(text, n_seq=1 << 16, threads=2, bloom_multiplier=1)
+    a4 = khhost.Addr(text, n_seq=1 << 16, threads=2, bloom_multiplier=4)
+    assert a1.bloom() == a4.bloom()
+    a1.close()
+    a4.close()

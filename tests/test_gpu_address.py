@@ -173,6 +173,29 @@ def test_cli_rmd160_compress_range(tmp_path, keys):
     assert "[+] Search compress only" in r.stdout
 
 
+def test_cli_bloom_multiplier(tmp_path, keys, ora):
+    """-z 4 with more than 10,000 targets (keyhunt.cpp:766-772, 6559-6576): the CLI prints the reference's
+    "[+] Bloom Size Multiplier 4" line and a target bloom of the oracle's bloom_init2(4 x items) size, and
+    still finds puzzle #20 planted among 12,000 synthetic hash160 lines."""
+    import random
+    rng = random.Random(9)
+    lines = ["%040x" % rng.getrandbits(160) for _ in range(12000)]
+    with open(os.path.join(GOLD, "address", "1to32.rmd")) as f:
+        p20 = f.read().split("\n")[19].strip()
+    lines.insert(6000, p20)
+    text = "\n".join(lines) + "\n"
+    (tmp_path / "t.rmd").write_text(text)
+    O = ora.AddrTable(text, bloom_multiplier=4)
+    mb = O.bloom().bytes / 1048576.0
+    O.close()
+    r = _cli(["-m", "rmd160", "-f", "t.rmd", "-b", "20", "-n", "0x100000", "-z", "4", "-q", "-s", "0"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "[+] Bloom Size Multiplier 4\n" in r.stdout
+    assert "[+] Loading data to the bloomfilter total: %.2f MB\n" % mb in r.stdout
+    k = int(keys["20"]["key"], 16)
+    assert f"Hit! Private Key: {k:x}\n" in r.stdout
+
+
 @pytest.mark.parametrize("search", [0, 1, 2])
 def test_addr_unsolvedpuzzles_bloom_matches_oracle(eng, ora, search):
     """Config E's own target file (tests/unsolvedpuzzles.rmd, sized by keyhunt.cpp:6559-6576 with its

@@ -220,8 +220,9 @@ def tables_k4():
 def test_k4_full_geometry_candidates_match_oracle(tables_k4, ora):
     """Config C (-k 4, default -n): 2^24 baby steps, 57.5 MiB level-1 bloom.  Every candidate of two
     whole chunks (2 x 1024 groups) equals the oracle's, and the key comes back through the second
-    check at k = 4 (M3 = 16384).  The level-0 gate's candidates are the same with and without its
-    stage-1 fold (khb_set_gate_stage1), a subset of the ungated ones, and still hold the key."""
+    check at k = 4 (M3 = 16384).  The level-0 gate's candidates are exactly the L1 candidates whose
+    gate bits are set (x from the GPU dump of their group), with no fold, a 32 MiB fold and the
+    product's auto 16 MiB fold (khb_set_gate_stage1), and still hold the key."""
     from keyhuntm1cpu_amd.khbsgs import Engine
     bs = ora.Bsgs(None, 4)
     assert bs.m == tables_k4.m == 1 << 24 and bs.cycles == tables_k4.cycles == 1024
@@ -244,8 +245,17 @@ def test_k4_full_geometry_candidates_match_oracle(tables_k4, ora):
             e.load_gate(gate, lg, tables_k4.gate_probes())
             gated[stage1], gdegen, _ = e.scan(centres, 0, tables_k4.cycles)
             assert not gdegen
-    assert sorted(gated[25]) == sorted(gated[0]) == sorted(gated[1])
-    assert set(gated[0]) <= set(got)
+        # exact: gated == {L1 candidate whose x passes the gate}, as test_full_geometry_gate at k = 1
+        cl = [tables_k4.chunk_centre(b, t.be64()) for b in bases]
+        exp = []
+        for j, a in got:
+            g0 = (a // 1024) // gpl * gpl
+            xs = e.dump_x(cl[j], g0, gpl)
+            xb = xs[32 * (a - g0 * 1024):32 * (a - g0 * 1024) + 32]
+            if gate_pass(gate, lg, tables_k4.gate_probes(), int.from_bytes(xb, "big")):
+                exp.append((j, a))
+    for stage1 in (0, 25, 1):
+        assert sorted(gated[stage1]) == sorted(exp), stage1
     assert any(tables_k4.secondcheck(bases[0], a, t.be64()) == key for jj, a in gated[25] if jj == 0)
     assert not degen
     for j, b in enumerate(bases):

@@ -81,3 +81,21 @@ def test_failing_rank_fails_the_launch():
     assert r.returncode == 3
     assert r.stdout.strip() == ""                              # no line when a rank failed
     assert "rank 2 exited with status 3" in r.stderr
+
+
+def test_straggler_rank_is_stopped():
+    """A rank that hangs after another rank exited cleanly is stopped after straggler_s:
+    the launch returns 124 instead of polling forever."""
+    code = ("import os, time, sys\n"
+            "time.sleep(3600 if os.environ['RANK'] == '1' else 0)\n")
+    import time
+    t0 = time.time()
+    rc = launch.spawn_ranks(2, [sys.executable, "-c", code], env=_clean_env(), grace_s=1.0, straggler_s=2.0)
+    assert rc == 124
+    assert time.time() - t0 < 30
+
+
+def test_overall_timeout_stops_ranks():
+    code = "import time\ntime.sleep(3600)\n"
+    rc = launch.spawn_ranks(2, [sys.executable, "-c", code], env=_clean_env(), grace_s=1.0, timeout_s=2.0)
+    assert rc == 124

@@ -41,7 +41,9 @@ step pmc write
 JOBS=$J GATE=1 ROUNDS=1 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE TCC_EA0_WRREQ_sum -d $O/pmc_write_0 -o pmc --output-format csv -- python3 tools/perf_variants.py $L > $O/pmc_write_0.log 2>&1 || exit 1
 step pmc sq
 JOBS=$J GATE=1 ROUNDS=1 timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU GRBM_GUI_ACTIVE -d $O/pmc_sq -o pmc --output-format csv -- python3 tools/perf_variants.py $L > $O/pmc_sq.log 2>&1 || exit 1
-for d in $O/pmc_fetch_0 $O/pmc_fetch_13 $O/pmc_write_0 $O/pmc_sq; do   # pmc_summary reads <dir>/pmc_counter_collection.csv
+step pmc sq2
+JOBS=$J GATE=1 ROUNDS=1 timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d $O/pmc_sq2 -o pmc --output-format csv -- python3 tools/perf_variants.py $L > $O/pmc_sq2.log 2>&1 || exit 1
+for d in $O/pmc_fetch_0 $O/pmc_fetch_13 $O/pmc_write_0 $O/pmc_sq $O/pmc_sq2; do   # pmc_summary reads <dir>/pmc_counter_collection.csv
   f=$(find $d -name "*counter_collection.csv" | sort | tail -1)
   [ "$f" = "$d/pmc_counter_collection.csv" ] || cp "$f" $d/pmc_counter_collection.csv
 done

@@ -76,6 +76,11 @@ def open_engine(p, gs):
 pipe = int(os.environ.get("PIPE", "0") or 0)
 times = {cfg_name(p, gs): [] for p, gs in configs}
 mhz = {n: [] for n in times}
+watts = {n: [] for n in times}
+# POWER=1: board power over each timed pipe (keyhuntm1cpu_amd/power.py; amdsmi, not HIP)
+use_power = os.environ.get("POWER", "0") == "1"
+if use_power:
+    from keyhuntm1cpu_amd.power import PowerSampler
 ncand = {}
 ref = {}
 for rnd in range(int(os.environ.get("ROUNDS", "3"))):
@@ -88,13 +93,21 @@ for rnd in range(int(os.environ.get("ROUNDS", "3"))):
                 print(f"{n}: lanes {e.lanes()}", flush=True)
             if pipe:
                 # PIPE=n: n launches with two in flight (the engine's queue depth), wall time per launch
+                ps = PowerSampler(period=0.02) if use_power else None
                 e.submit(centres, 0, t.cycles)
+                if ps:
+                    ps.__enter__()
                 t0 = time.perf_counter()
                 for _ in range(pipe - 1):
                     e.submit(centres, 0, t.cycles)
                     c, d, st = e.collect()
                 c, d, st = e.collect()
                 kms = 1e3 * (time.perf_counter() - t0) / pipe
+                if ps:
+                    ps.__exit__(None, None, None)
+                    sm = ps.summary()
+                    watts[n].append((sm.get("power_w_from_energy") or sm.get("power_w_avg") or 0.0,
+                                     sm.get("ppt_residency_frac")))
             else:
                 c, d, st = e.scan(centres, 0, t.cycles)
                 kms = st.kernel_ms
@@ -117,5 +130,11 @@ for g in ref:   # a gate keeps a subset of the L1 candidates
 steps = jobs * t.cycles * 1024
 for n in times:
     med = statistics.median(times[n])
+    pw = ""
+    if watts[n]:
+        w = statistics.median(x[0] for x in watts[n])
+        ppt = [x[1] for x in watts[n] if x[1] is not None]
+        pw = (f"  {w:7.1f} W  {w * med * 1e-3 / (steps / 1e9):6.2f} J/1e9 steps"
+              + (f"  ppt {statistics.median(ppt):.3f}" if ppt else ""))
     print(f"{n:48s} median {med:8.2f} ms  min {min(times[n]):8.2f}  {steps / med / 1e6:8.3f} G steps/s"
-          f"  cand {ncand[n]}  clock {statistics.median(mhz[n]):7.1f} MHz", flush=True)
+          f"  cand {ncand[n]}  clock {statistics.median(mhz[n]):7.1f} MHz{pw}", flush=True)

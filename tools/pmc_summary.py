@@ -7,12 +7,22 @@ geometry; the tiny first dispatch of perf_variants is skipped):
   pmc_fetch_13  the same launches plus the all-zero 1 KiB gate's (no gate traffic)
   pmc_write_0   WRITE_SIZE, TCC_EA0_WRREQ_sum
   pmc_sq        SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE, ...
+  pmc_sq2       (round 5, optional) SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, SQ_ACTIVE_INST_VALU2, SQ_INSTS_VALU_INT32/64,
+                SQ_BUSY_CYCLES, SQ_WAVE_CYCLES, GRBM_GUI_ACTIVE: the VALU utilisation below
 Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half of a wide coalesced
 streaming read, so the prefix stream's read bytes are 2 x the zero-gate launch's FETCH_SIZE;
 WRITE_SIZE is exact for the 16-B-per-lane prefix stores.  The gate's reads are the extra memory-side
 read requests of the real-gate launch (TCC_EA0_RDREQ real - zero) x 64 B (FETCH_SIZE = RDREQ x 64 B;
 the scattered 8-B probe's request width is not calibrated, and Infinity-Cache hits are counted with
 HBM reads: these are memory-side bytes, HBM or MALL).
+VALU utilisation: a SIMD issues one VALU wave-instruction per quad-cycle, or two from different
+waves when both are dual-issuable (SQ_ACTIVE_INST_VALU2 counts those quad-cycles).  SQ_ACTIVE_INST_VALU counts one
+quad-cycle per VALU instruction (it equals SQ_INSTS_VALU here), so the quad-cycles in which the SIMD issued VALU
+work are ACTIVE_INST_VALU - ACTIVE_INST_VALU2, and
+  valu_util_pct = (ACTIVE_INST_VALU - ACTIVE_INST_VALU2) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs / 4)
+is the share of the launch's SIMD quad-cycles that issued VALU work (<= 100 % by construction).  The 4-cycle model
+(rocprof's VALUBusy, ACTIVE_INST_VALU x 4 / SIMDs / per-XCD GRBM_GUI_ACTIVE) counts a dual-issued pair twice and
+reads above 100 % (valu_busy_pct, kept for comparison).
 Usage: python tools/pmc_summary.py <dir with the pmc_* subdirs> <chunks per launch> [out.json]"""
 import collections
 import csv
@@ -47,7 +57,9 @@ def main():
     gate_rd = (real_f["TCC_EA0_RDREQ_sum"] - zero_f["TCC_EA0_RDREQ_sum"]) * 64
     xcds = 8
     out = {
-        "kernel": "k_giant_scan", "k": 1, "chunks_per_launch": chunks, "giant_steps_per_launch": steps,
+        "kernel": "k_giant_scan", "k": 1, "level0_gate": True, "lanes": int(os.environ.get("LANES", "262144")),
+        "waves_per_simd": int(os.environ.get("WAVES", "4")),
+        "chunks_per_launch": chunks, "giant_steps_per_launch": steps,
         "fetch_size_kib_real_gate": real_f["FETCH_SIZE"], "fetch_size_kib_zero_gate": zero_f["FETCH_SIZE"],
         "write_size_kib": real_w["WRITE_SIZE"],
         "ea_rdreq_real_gate": real_f["TCC_EA0_RDREQ_sum"], "ea_rdreq_zero_gate": zero_f["TCC_EA0_RDREQ_sum"],
@@ -69,6 +81,19 @@ def main():
                 "Infinity-Cache hits from HBM. VALUBusy = ACTIVE_INST_VALU x 4 / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 XCDs).",
         "source": os.path.relpath(src, REPO),
     }
+    sq2_dir = os.path.join(src, "pmc_sq2")
+    if os.path.isdir(sq2_dir):
+        q = dispatches(sq2_dir)[-1]
+        quads = 1024 * q["GRBM_GUI_ACTIVE"] / xcds / 4
+        out.update({
+            "valu_util_pct": round(100 * (q["SQ_ACTIVE_INST_VALU"] - q["SQ_ACTIVE_INST_VALU2"]) / quads, 2),
+            "valu_dual_issue_frac": round(2 * q["SQ_ACTIVE_INST_VALU2"] / q["SQ_INSTS_VALU"], 4),
+            "valu_int32_frac": round(q["SQ_INSTS_VALU_INT32"] / q["SQ_INSTS_VALU"], 4),
+            "valu_int64_frac": round(q["SQ_INSTS_VALU_INT64"] / q["SQ_INSTS_VALU"], 4),
+            "valu_util_basis": "(SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) / SIMD quad-cycles (1024 SIMDs x "
+                               "GRBM_GUI_ACTIVE / 8 XCDs / 4): the share of quad-cycles issuing VALU work, dual-issued "
+                               "pairs counted once",
+            "valu_util_source": os.path.relpath(sq2_dir, REPO)})
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
         f.write("\n")
