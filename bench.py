@@ -191,10 +191,11 @@ def main():
                          "eight work items (4096 at k=1, 16384 at k=4), as the CLI's auto batch does "
                          "(engine.cpp batch_chunks)")
     ap.add_argument("--k", type=int, default=1)
-    ap.add_argument("--cpu-seconds", type=float, default=60.0,
-                    help="CPU-baseline window after the table build (SURVEY.md section 8d: 60 s)")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0,
+                    help="CPU-baseline window after the table build (default 3 windows of 20 s: SURVEY.md section 8d's "
+                         "60 s, with the spread between windows)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-windows", type=int, default=1,
+    ap.add_argument("--cpu-windows", type=int, default=3,
                     help="repeat the CPU-baseline window this many times and report the mean and spread")
     ap.add_argument("--no-power", action="store_true", help="do not sample board power during the timed region")
     ap.add_argument("--share-gpus", action="store_true",

@@ -11,7 +11,9 @@ fallback for the giant-step scan: loading fails loudly when the native library i
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_DIR = os.path.join(PKG_DIR, "lib")
+# KHB_LIB_DIR: another directory holding a libkhbsgs.so + libkhhost.so pair (whole-bench A/B of a kernel build,
+# tools/gpu/bench_ab.sh); the in-tree lib/ otherwise
+LIB_DIR = os.environ.get("KHB_LIB_DIR") or os.path.join(PKG_DIR, "lib")
 BIN_DIR = os.path.join(PKG_DIR, "bin")
 REPO_DIR = os.path.dirname(PKG_DIR)
 

@@ -44,11 +44,6 @@ constexpr uint32_t kBlock = 256;
 #define KHB_BATCH 8               // -m bsgs groups per work item (scan_batch): two inversions per item
 #endif
 constexpr uint32_t kBatch = KHB_BATCH;
-#ifndef KHB_HALF_STREAM
-// 1: the forward pass stores only the odd prefixes P_1, P_3, ..., P_509 and the walk rebuilds each even one
-// from its odd neighbour (one extra product per two walk steps, half the prefix stream)
-#define KHB_HALF_STREAM 0
-#endif
 
 // Kernel modes (template argument of scan_group / k_giant_scan).
 enum : int {
@@ -626,84 +621,6 @@ __device__ __forceinline__ void walk_group_g(const ScanArgs& A, ProbeQueue& Q, c
   probe<false>(A, Q, C.x, job, j, kHalf);        // the centre, pts[512]
 }
 
-// walk_group_g over the half prefix stream (KHB_HALF_STREAM): the forward pass stored only the odd prefixes.
-// After the peeled step 511 the walk goes in pairs (even i, odd i - 1): the even step needs P_{i-1}, stored,
-// and then loads P_{i-3}; the odd step rebuilds P_{i-2} = P_{i-3} * dx_{i-2} (one extra product per pair).
-// Same points, same order and bit-identical x: P_{i-2} is the forward pass's own product of the same
-// operands in the same order.
-template <bool STAGE1>
-__device__ __forceinline__ void half_points(const ScanArgs& A, ProbeQueue& Q, const AffPt& C, const Fe& negCx,
-                                            const Fe& negCy, const Fe& idx, int i, uint32_t base, uint32_t job) {
-  const GsnTable gsn{A.gsn};
-  Fe u, s, x1, x2;
-  const AffPt g = gsn.pt(i);
-  fm_add_lazy(u, gsn.nx(i), negCx);             // nu = -(C.x + GSn.x)
-  fm_add_lazy(s, g.y, C.y);
-  fm_mul(s, s, idx);
-  fm_sqr_add(x1, s, u);
-  x_out<kScanG>(A, x1);
-  fm_add_lazy(s, g.y, negCy);
-  fm_mul(s, s, idx);
-  fm_sqr_add(x2, s, u);
-  x_out<kScanG>(A, x2);
-  gate_pair<STAGE1>(A, Q, x1, base + kHalf - 1 - (uint32_t)i, true, x2, base + kHalf + 1 + (uint32_t)i, job);
-}
-
-template <bool STAGE1>
-__device__ __forceinline__ void walk_group_g_half(const ScanArgs& A, ProbeQueue& Q, const AffPt& C, Fe inv,
-                                                  uint32_t job, uint32_t j, const Fe* scr) {
-  const size_t S = A.stride;
-  const GsnTable gsn{A.gsn};
-  const uint32_t base = j * KHB_GROUP;
-  Fe negCx, negCy;
-  {
-    Fe p;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) p.v[k] = k == 0 ? KHB_P0 : (k == 1 ? KHB_P1 : 0xFFFFFFFFu);
-    fm_sub(negCx, p, C.x);
-    fm_sub(negCy, p, C.y);
-  }
-  Fe pre = scr_ld(scr + (size_t)(kHalf - 3) * S);          // P_509
-  Fe idx, dx;
-  // odd step 511: pts[0] = C - GSn[511] only
-  {
-    Fe u, s, x1;
-    fm_add_lazy(dx, gsn.x(kHalf - 2), negCx);
-    fm_mul(idx, pre, dx);                                  // P_510 = P_509 * dx_510
-    fm_mul(idx, inv, idx);
-    fm_add_lazy(dx, gsn.x(kHalf - 1), negCx);
-    fm_mul(inv, inv, dx);
-    const AffPt g = gsn.pt(kHalf - 1);
-    fm_add_lazy(u, gsn.nx(kHalf - 1), negCx);
-    fm_add_lazy(s, g.y, C.y);
-    fm_mul(s, s, idx);
-    fm_sqr_add(x1, s, u);
-    x_out<kScanG>(A, x1);
-    gate_pair<STAGE1>(A, Q, x1, base, false, x1, 0, job);
-  }
-  // pairs (even i, odd i - 1), i = 510 ... 2; pre = P_{i-1} on entry
-  for (int i = (int)kHalf - 2; i >= 2; i -= 2) {
-    fm_mul(idx, inv, pre);                                 // even step i: P_{i-1} (odd index, stored)
-    if (i > 2) pre = scr_ld(scr + (size_t)(i - 3) * S);    // P_{i-3} for step i - 1 (and i - 2)
-    fm_add_lazy(dx, gsn.x(i), negCx);
-    fm_mul(inv, inv, dx);
-    half_points<STAGE1>(A, Q, C, negCx, negCy, idx, i, base, job);
-    // odd step i - 1: P_{i-2} = P_{i-3} * dx_{i-2} (i - 1 = 1: P_0 = dx_0)
-    fm_add_lazy(dx, gsn.x(i - 2), negCx);
-    if (i > 2) {
-      fm_mul(idx, pre, dx);
-      fm_mul(idx, inv, idx);
-    } else {
-      fm_mul(idx, inv, dx);
-    }
-    fm_add_lazy(dx, gsn.x(i - 1), negCx);
-    fm_mul(inv, inv, dx);
-    half_points<STAGE1>(A, Q, C, negCx, negCy, idx, i - 1, base, job);
-  }
-  half_points<STAGE1>(A, Q, C, negCx, negCy, inv, 0, base, job);     // step 0: idx = inv
-  probe<false>(A, Q, C.x, job, j, kHalf);
-}
-
 // One reference group centred on C, walked on its own (-m address, baby steps): the 513-element
 // batch of IntGroup.cpp:36-58 including dx[512] = _2GSn.x - C.x, whose inverse advances C to the
 // next centre (keyhunt.cpp:3986-3999).  For -m address this is keyhunt.cpp:2586-2711 with the
@@ -900,11 +817,11 @@ __device__ __forceinline__ uint32_t scan_batch(const ScanArgs& A, ProbeQueue& Q,
     }
     // dx_i = GSn[i].x - C.x as the lazy sum GSn[i].x + (p - C.x) (congruent; feeds products only)
     fm_add_lazy(a, gsn.x(0), negCx);
-    if (!(is_gated(MODE) && KHB_HALF_STREAM)) scr_st(sg, a);
+    scr_st(sg, a);
     for (uint32_t i = 1; i < kHalf - 1; ++i) {
       fm_add_lazy(dx, gsn.x(i), negCx);
       fm_mul(a, a, dx);
-      if (!(is_gated(MODE) && KHB_HALF_STREAM) || (i & 1u)) scr_st(sg + i * S, a);
+      scr_st(sg + i * S, a);
     }
     fm_add_lazy(dx, gsn.x(kHalf - 1), negCx);
     fm_mul(a, a, dx);
@@ -938,9 +855,7 @@ __device__ __forceinline__ uint32_t scan_batch(const ScanArgs& A, ProbeQueue& Q,
     Fe* const sg = scr + (size_t)g * kHalf * S;
     asm volatile("" ::: "memory");
     const AffPt C{sc[2 * g * S], sc[(2 * g + 1) * S]};
-    if constexpr (is_gated(MODE) && KHB_HALF_STREAM)
-      walk_group_g_half<MODE == kScanG1>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
-    else if constexpr (is_gated(MODE))
+    if constexpr (is_gated(MODE))
       walk_group_g<MODE == kScanG1>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
     else
       walk_group<MODE>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);

@@ -128,3 +128,56 @@ def test_bench_traffic_matches_default_batch():
     half = bench.pmc_traffic(pmc, auto // 2, steps // 2)
     assert abs(half["traffic"] - pmc["hbm_bytes_per_launch"] / 2) < 1e-3 * pmc["hbm_bytes_per_launch"]
     assert "scaled to 2048" in half["traffic_note"]
+
+
+def test_pmc_summary_valu_utilisation(tmp_path):
+    """The round-5 VALU utilisation: quad-cycles that issued VALU work (dual-issued pairs counted once) over
+    the SIMD quad-cycles of the launch; 900 instructions with 100 dual-issued pairs in 1000 quad-cycles per
+    SIMD -> 80 %, while the 4-cycle model reads 90 %."""
+    chunks = 1
+    steps = chunks * 4096 * 1024
+    quads_per_simd = 1000.0
+    insts = 900.0 * 1024
+    base = {"FETCH_SIZE": 1.0, "TCC_EA0_RDREQ_sum": 1.0}
+    _pmc(tmp_path / "pmc_fetch_0", [(1, base)])
+    _pmc(tmp_path / "pmc_fetch_13", [(1, base), (2, base)])
+    _pmc(tmp_path / "pmc_write_0", [(1, {"WRITE_SIZE": 1.0, "TCC_EA0_WRREQ_sum": 1.0})])
+    grbm = 8 * quads_per_simd * 4
+    _pmc(tmp_path / "pmc_sq", [(1, {"SQ_INSTS_VALU": insts, "SQ_ACTIVE_INST_VALU": insts, "GRBM_GUI_ACTIVE": grbm})])
+    _pmc(tmp_path / "pmc_sq2", [(1, {"SQ_INSTS_VALU": insts, "SQ_ACTIVE_INST_VALU": insts,
+                                     "SQ_ACTIVE_INST_VALU2": 100.0 * 1024, "SQ_INSTS_VALU_INT32": insts / 2,
+                                     "SQ_INSTS_VALU_INT64": insts / 4, "GRBM_GUI_ACTIVE": grbm})])
+    out = tmp_path / "pmc.json"
+    subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"), str(tmp_path), str(chunks),
+                    str(out)], capture_output=True, text=True, check=True)
+    d = json.loads(out.read_text())
+    assert d["valu_busy_pct"] == 90.0
+    assert d["valu_util_pct"] == 80.0
+    assert d["valu_dual_issue_frac"] == round(200 / 900, 4)
+    assert d["valu_int32_frac"] == 0.5 and d["valu_int64_frac"] == 0.25
+    assert steps
+
+
+def test_power_summary_synthetic():
+    """keyhuntm1cpu_amd/power.py's summary on synthetic samples (no amdsmi): averages, the cap fraction, energy
+    per 1e9 units from the energy counter, the throttle-residency fractions; a disabled sampler reports why."""
+    sys.path.insert(0, REPO)
+    from keyhuntm1cpu_amd.power import PowerSampler
+    ps = PowerSampler.disabled("test")
+    assert ps.summary() == {"available": False, "error": "test"}
+    ps = PowerSampler.disabled("test")
+    ps.err, ps.cap_w, ps.period = None, 1400.0, 0.05
+    ps.samples = [{"t": float(i), "power_w": w, "gfxclk": [2100.0, 2200.0], "gfx_activity": 100.0,
+                   "temp_hotspot": 50.0 + i, "temp_mem": 40.0, "throttle": "N/A", "indep_throttle": "N/A"}
+                  for i, w in enumerate((1300.0, 1400.0, 1350.0))]
+    ps._e0, ps._e1 = (0.0, 1000.0), (2.0, 3700.0)
+    ps._r0 = {"ppt_residency_acc": 10.0, "socket_thm_residency_acc": 0.0, "vr_thm_residency_acc": 0.0,
+              "hbm_thm_residency_acc": 0.0, "prochot_residency_acc": 0.0, "accumulation_counter": 100.0}
+    ps._r1 = dict(ps._r0, ppt_residency_acc=90.0, accumulation_counter=200.0)
+    s = ps.summary(work_units=27e9, seconds=2.0)
+    assert s["power_w_avg"] == 1350.0 and s["gfxclk_mhz_avg"] == 2150.0
+    assert s["power_w_from_energy"] == 1350.0 and s["energy_j"] == 2700.0
+    assert s["at_cap_frac"] == round(1350 / 1400, 3)
+    assert s["joules_per_1e9_giant_steps"] == 100.0
+    assert s["ppt_residency_frac"] == 0.8 and s["prochot_residency_frac"] == 0.0
+    assert "throttle_status_seen" not in s

@@ -14,7 +14,8 @@
 #   addrwalk_patch.py: the -m address kernels without the hashing (count-only: the x/y walk's VALU).
 #   plainscr_patch.py: the prefix-scratch stream with plain loads and stores (the product's are non-temporal).
 #   fold2_patch.py: the stage-1 gate fold tested with two of the three probes (candidates unchanged).
-# Usage: tools/experiments/calib_build.sh pad|rm|scr|pair|defer|nonop|block|addrwalk|plainscr|fold2 <name> [-DKEY=VAL ...]
+#   half_patch.py: the half prefix stream (exact; tools/experiments/half_stream.hpp, round 5).
+# Usage: tools/experiments/calib_build.sh pad|rm|scr|pair|defer|nonop|block|addrwalk|plainscr|fold2|half <name> [-DKEY=VAL ...]
 set -e
 KIND=$1; NAME=$2; shift 2
 S1=keyhuntm1cpu_amd/csrc/device/fe_asm.hpp
