@@ -145,6 +145,15 @@ def power_sampler(torch, local: int, args):
     return PowerSampler(bus)
 
 
+def physical_gpu(torch, local: int) -> str:
+    """The PCI address of this rank's GPU (ranks on the same physical GPU report the same string)."""
+    try:
+        p = torch.cuda.get_device_properties(local)
+        return "%04x:%02x:%02x" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+    except Exception:                                  # noqa: BLE001
+        return "device%d" % local
+
+
 def init_gloo(dist, rank: int, world: int):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     # gloo's C++ connect messages go to fd 1; keep stdout for the one JSON line (rank 0)
@@ -228,20 +237,27 @@ def main():
     import torch                                   # first: share torch's HIP runtime with our libraries
     import torch.distributed as dist
     ndev = torch.cuda.device_count()
-    shared = bool(ndev) and world > ndev
     if ndev and local >= ndev:
-        if not args.share_gpus:
-            # a line from ranks sharing GPUs would read as an N-GPU measurement: refuse
-            raise SystemExit(f"[bench] rank {rank}: LOCAL_RANK {local} >= {ndev} visible GPUs; pass --share-gpus for a "
-                             f"multi-rank rehearsal on fewer GPUs")
-        # more ranks than visible GPUs (a multi-rank rehearsal on a smaller box): share round-robin
-        print(f"[bench] rank {rank}: LOCAL_RANK {local} >= {ndev} visible GPUs, using GPU {local % ndev}",
-              file=sys.stderr, flush=True)
+        # fewer visible GPUs than this LOCAL_RANK: either a launcher that shows each rank its own GPU only
+        # (then device 0 is this rank's), or more ranks than GPUs (a rehearsal) -- told apart below
         local = local % ndev
-    gpu_info = {"physical_gpus": min(world, ndev) if ndev else world, "gpus_shared": shared}
     torch.cuda.set_device(local)
+    gpu_id = physical_gpu(torch, local)
+    ids = [gpu_id]
     if world > 1:
         init_gloo(dist, rank, world)
+        ids = [None] * world
+        dist.all_gather_object(ids, gpu_id)
+    physical = len(set(ids))
+    gpu_info = {"physical_gpus": physical, "gpus_shared": physical < world}
+    if physical < world:
+        # a line from ranks sharing GPUs would read as an N-GPU measurement: refuse unless asked
+        msg = (f"[bench] {world} ranks on {physical} physical GPU(s) (PCI {sorted(set(ids))})")
+        if not args.share_gpus:
+            if world > 1:
+                dist.destroy_process_group()
+            raise SystemExit(msg + "; pass --share-gpus for a multi-rank rehearsal on fewer GPUs")
+        print(msg + ": a rehearsal (--share-gpus); the line says gpus_shared", file=sys.stderr, flush=True)
 
     from keyhuntm1cpu_amd import khhost
     from keyhuntm1cpu_amd.partition import blocks_fit, fit_batch, rank_range
