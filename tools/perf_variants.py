@@ -138,3 +138,5 @@ for n in times:
               + (f"  ppt {statistics.median(ppt):.3f}" if ppt else ""))
     print(f"{n:48s} median {med:8.2f} ms  min {min(times[n]):8.2f}  {steps / med / 1e6:8.3f} G steps/s"
           f"  cand {ncand[n]}  clock {statistics.median(mhz[n]):7.1f} MHz{pw}", flush=True)
+for n in times:
+    print(f"  {n}: rounds (ms) {[round(x, 2) for x in times[n]]}", flush=True)
