@@ -388,8 +388,9 @@ def main():
         print(f"[bench] ERROR: device-busy {bmax:.3f} ms per step exceeds the wall time {wall_ms:.3f} ms",
               file=sys.stderr, flush=True)
         raise SystemExit(3)
-    time_basis = ("kernel_busy_ms_per_step: union of the k_giant_scan launch intervals over the timed "
-                  "steps (HIP events on each launch's stream) / steps; <= ms_per_step")
+    time_basis = ("kernel_busy_ms_per_step: union of the k_giant_scan launch intervals over the timed steps / steps "
+                  "(each launch's execution span on the device's 100 MHz clock, ending at its end event on the "
+                  "launch's stream); <= ms_per_step")
     if bmax <= 0:    # no launch interval was timed (events unavailable): fall back to the wall time
         bmax = wall_ms
         time_basis = "ms_per_step (the launches' event intervals were unavailable)"

@@ -206,3 +206,35 @@ def test_engine_falls_back_to_depth_one():
         assert st["launches"] >= 3                   # [2^25, 2^28) is 7 chunks of 2N = 2^25: 4 batches
     finally:
         t.close()
+
+
+def test_lazy_second_slot_under_a_full_residency_launch():
+    """Round 5's host hand-over (launch epilogue, counters zeroed by the kernel): a small warm-up launch, then a
+    full-residency launch on slot 0 with the second slot allocated while it runs.  The second slot's counters are
+    zeroed on its own stream (a null-stream hipMemset queued behind the running launch zeroed them mid-launch
+    and re-walked 6,144 groups: tools/debug/epilogue_diag.py).  Every collect has the submitted walked count, and
+    the execution span (khb_stats.kernel_ms) is positive and no longer than the launch's events."""
+    import ctypes as C
+    from keyhuntm1cpu_amd.khbsgs import Engine, Cand, Degenerate, Stats
+    t = khhost.Tables(None, 1, threads=16)
+    tgt = khhost.pubkey(0x2832ED74F2B5E35EE)
+    jobs = 512
+    centres = b"".join(t.chunk_centre((1 << 65) + c * (1 << 45), tgt) for c in range(jobs))
+    with Engine(0) as e:
+        bf, nb, bits, h = t.bloom_concat(1)
+        e.load_bloom(bf, nb, bits, h)
+        gate, lg = t.gate()
+        e.load_gate(gate, lg, t.gate_probes())
+        e.load_giant_table(t.giant_table())
+        offs, gpl = t.lane_offsets()
+        e.load_lane_offsets(offs, gpl)
+        e.scan(centres[:64 * 8], 0, 64)                 # warm-up: small, slot 0
+        e.submit(centres, 0, t.cycles)                   # slot 0, full residency
+        e.submit(centres, 0, t.cycles)                   # slot 1 allocated now, while slot 0 runs
+        for _ in range(2):
+            cand, deg, st = (Cand * 4096)(), (Degenerate * 4096)(), Stats()
+            rc = e.L.khb_collect(e.h, cand, 4096, deg, 4096, C.byref(st))
+            assert rc == 0 and st.giant_steps == jobs * t.cycles * 1024, (rc, st.giant_steps)
+            assert 0 < st.kernel_ms and st.launch_end_ms - st.launch_begin_ms == pytest.approx(st.kernel_ms, abs=1e-3)
+            assert 1000 < st.shader_mhz < 3000
+    t.close()
