@@ -107,7 +107,8 @@ def test_committed_pmc_latest_reproduces_from_its_csvs(tmp_path):
                     str(cur["chunks_per_launch"]), str(out)], capture_output=True, text=True, check=True)
     again = json.loads(out.read_text())
     for k in ("hbm_bytes_per_launch", "bytes_per_giant_step", "gate_read_requests_per_giant_step",
-              "valu_instr_per_giant_step"):
+              "valu_instr_per_giant_step", "valu_util_pct", "valu_dual_issue_frac", "level0_gate", "lanes",
+              "waves_per_simd"):
         assert again[k] == cur[k], k
     assert pmc_summary.GROUPS == 4096
 
