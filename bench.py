@@ -69,6 +69,17 @@ def pmc_traffic(pmc: dict, chunks: int, launch_steps: int) -> dict:
                             % (pmc["chunks_per_launch"], chunks)}
 
 
+def pmc_mismatch(pmc: dict, run_cfg: dict) -> str | None:
+    """None when profiles/pmc_latest.json was measured on this run's kernel configuration (k, level-0 gate, lanes,
+    waves per SIMD; a key the record lacks counts as a mismatch), else the note the line carries instead of the
+    traffic and VALU figures (a --no-gate or other-build run must not borrow them)."""
+    mism = {key: (pmc.get(key), v) for key, v in run_cfg.items() if pmc.get(key) != v}
+    if not mism:
+        return None
+    return ("profiles/pmc_latest.json was measured for another configuration (%s); traffic not measured for this run"
+            % ", ".join("%s %s vs %s" % (k, a, b) for k, (a, b) in mism.items()))
+
+
 def mulops_peak_t(ghz: float) -> float:
     return round(PEAK_LANES_PER_CLK_CU * CUS * ghz * 1e9 / 1e12, 2)
 
@@ -428,12 +439,10 @@ def main():
             with open(pmc_path) as f:
                 pmc = json.load(f)
             # the PMC record applies only to the kernel it was measured on
-            run_cfg = {"k": args.k, "level0_gate": not args.no_gate, "lanes": lanes, "waves_per_simd": waves}
-            mism = {key: (pmc.get(key), v) for key, v in run_cfg.items() if pmc.get(key) != v}
-            if mism:
-                roofline["traffic_note"] = ("profiles/pmc_latest.json was measured for another configuration "
-                                            "(%s); traffic not measured for this run" %
-                                            ", ".join("%s %s vs %s" % (k_, a, b) for k_, (a, b) in mism.items()))
+            note = pmc_mismatch(pmc, {"k": args.k, "level0_gate": not args.no_gate, "lanes": lanes,
+                                      "waves_per_simd": waves})
+            if note:
+                roofline["traffic_note"] = note
             else:
                 roofline.update(pmc_traffic(pmc, args.chunks, per_launch_steps))
                 roofline["traffic_source"] = os.path.relpath(pmc_path, REPO)

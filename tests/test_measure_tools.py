@@ -182,3 +182,19 @@ def test_power_summary_synthetic():
     assert s["joules_per_1e9_giant_steps"] == 100.0
     assert s["ppt_residency_frac"] == 0.8 and s["prochot_residency_frac"] == 0.0
     assert "throttle_status_seen" not in s
+
+
+def test_pmc_record_attaches_only_to_its_configuration():
+    """bench.py attaches profiles/pmc_latest.json's traffic / VALU figures only to a run of the kernel configuration
+    the record was measured on: the committed record matches the default k=1 gated 4-wave line, and a
+    --no-gate, k=4 or other-lane-count run gets a note instead."""
+    sys.path.insert(0, REPO)
+    import bench
+    with open(os.path.join(REPO, "profiles", "pmc_latest.json")) as f:
+        pmc = json.load(f)
+    default = {"k": 1, "level0_gate": True, "lanes": 262144, "waves_per_simd": 4}
+    assert bench.pmc_mismatch(pmc, default) is None
+    for change in ({"level0_gate": False}, {"k": 4}, {"lanes": 196608, "waves_per_simd": 3}):
+        note = bench.pmc_mismatch(pmc, dict(default, **change))
+        assert note and "not measured for this run" in note and all(k in note for k in change)
+    assert bench.pmc_mismatch({"k": 1}, default)          # a record without its configuration never matches
