@@ -16,7 +16,8 @@
 #   fold2_patch.py: the stage-1 gate fold tested with two of the three probes (candidates unchanged).
 #   half_patch.py: the half prefix stream (exact; tools/experiments/half_stream.hpp, round 5).
 #   scrplain_patch.py: scr_patch with plain accesses (the stream cache-resident; scr2plain / scr1plain, round 5).
-# Usage: tools/experiments/calib_build.sh pad|rm|scr|pair|defer|nonop|block|addrwalk|plainscr|fold2|half|scrplain <name> [-DKEY=VAL ...]
+#   early_patch.py: the first x's stage-1 fold load issued before the second x is computed (round 5).
+# Usage: tools/experiments/calib_build.sh pad|rm|scr|pair|defer|nonop|block|addrwalk|plainscr|fold2|half|scrplain|early <name> [-DKEY=VAL ...]
 set -e
 KIND=$1; NAME=$2; shift 2
 S1=keyhuntm1cpu_amd/csrc/device/fe_asm.hpp
