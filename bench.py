@@ -362,18 +362,20 @@ def main():
     waves = lanes // (torch.cuda.get_device_properties(local).multi_processor_count * 4 * 64)
     per_launch_steps = args.chunks * tables.cycles * 1024
     kernel_ms = 1e3 * st["kernel_s"] / max(1, st["launches"])
+    event_ms = 1e3 * st["event_s"] / max(1, st["launches"])     # dispatch to end, as rocprofv3's trace
     # device-busy time per step: the union of this rank's launch intervals (HIP events on each launch's
     # stream, khb_stats.launch_begin_ms/end_ms) over the timed region, per step
     busy_ms = 1e3 * st["busy_s"] / args.steps
     bad_count = 0.0 if steps_done == args.steps * per_launch_steps and st["rescans"] == 0 else 1.0
     tot_steps, tmax, kmax, bmax, bad = steps_done, dt, kernel_ms, busy_ms, bad_count
     if world > 1:
-        v = torch.tensor([float(steps_done), dt, kernel_ms, busy_ms, bad_count], dtype=torch.float64)
+        v = torch.tensor([float(steps_done), dt, kernel_ms, busy_ms, bad_count, event_ms], dtype=torch.float64)
         s = v.clone()
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         m = v.clone()
         dist.all_reduce(m, op=dist.ReduceOp.MAX)
         tot_steps, tmax, kmax, bmax, bad = s[0].item(), m[1].item(), m[2].item(), m[3].item(), m[4].item()
+        event_ms = m[5].item()
     if bad or tot_steps != world * args.steps * per_launch_steps:
         # a line over an incomplete or repeated count is never printed (every rank exits non-zero)
         print(f"[bench] ERROR: the device counted {tot_steps:.0f} giant steps over the ranks, "
@@ -419,6 +421,11 @@ def main():
                 "kernel_busy_ms_per_step": round(bmax, 3),
                 "shader_mhz_avg": round(mhz, 1),
                 "kernel_ms_avg": round(kmax, 3),
+                "kernel_event_ms_avg": round(event_ms, 3),
+                "kernel_ms_basis": "kernel_ms_avg: a launch's execution span (its first workgroup's start to its "
+                                   "last wave's exit); kernel_event_ms_avg: its HIP events, dispatch to end, the "
+                                   "duration rocprofv3 --kernel-trace reports, which with two launches in flight "
+                                   "includes the wait behind the other slot's launch (DESIGN.md §5)",
                 "achieved_per_launch": round(achieved_launch, 3),
                 "frac_per_launch": round(achieved_launch / PEAK_MULOPS_T, 4),
                 "peak_basis": "v_mad_u64_u32 %.1f lane-ops/clk/CU (profiles/r01_intops2.txt) x %d CUs at the %.1f GHz "

@@ -44,8 +44,8 @@ extern "C" {
 /* ABI version of this header (entry points, khb_stats and the other structs); bumped whenever one of
  * them changes.  A binding checks khb_abi_version() == the KHB_ABI_VERSION it was written for before
  * any other call (khb_stats gained launch_begin_ms/launch_end_ms/shader_mhz in ABI 3 and 4; ABI 5 added
- * khb_load_check_tables / khb_check). */
-#define KHB_ABI_VERSION 5
+ * khb_load_check_tables / khb_check; ABI 6 added khb_stats.event_ms). */
+#define KHB_ABI_VERSION 6
 int khb_abi_version(void);
 
 typedef struct khb_ctx khb_ctx;
@@ -79,6 +79,9 @@ typedef struct {
   double launch_end_ms;    /* overlap, so the union of these intervals is the device-busy time. */
   float shader_mhz;        /* average shader clock over the launch (s_memtime / s_memrealtime from its first
                               wave's start to its last wave's exit), 0 if unavailable */
+  float event_ms;          /* the submission's HIP-event time, dispatch to end: the launch duration
+                              rocprofv3 --kernel-trace reports (>= kernel_ms; with two submissions in flight
+                              it includes the wait behind the other slot's launch), -1 if unavailable */
 } khb_stats;
 
 /* ---- device / context ---- */

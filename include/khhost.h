@@ -79,8 +79,10 @@ int khh_search(const khh_tables* t, const uint8_t* targets_xy, int n_targets, co
  * rescanned in parts after a candidate-ring overflow, [7]=device-busy microseconds (union of each
  * device's launch intervals, summed over devices; two launches in flight overlap, so [7] <= [4]),
  * [8]=average shader clock of the launches in kHz, [9]=candidates confirmed on the GPU (khb_check),
- * [10]=microseconds spent in those khb_check calls. */
-#define KHH_SESSION_STATS 11
+ * [10]=microseconds spent in those khb_check calls, [11]=the launches' summed HIP-event microseconds
+ * (khb_stats.event_ms: dispatch to end, what rocprofv3's kernel trace reports; [4] sums their execution
+ * spans, khb_stats.kernel_ms). */
+#define KHH_SESSION_STATS 12
 typedef struct khh_session khh_session;
 khh_session* khh_session_open(const khh_tables* t, const int* devices, int n_devices, uint32_t lanes,
                               uint32_t chunks_per_batch, int check_threads, char* err, size_t errlen);

@@ -444,6 +444,7 @@ void device_thread(Shared& S, khb_ctx* ctx) {
       std::lock_guard<std::mutex> lk(S.mu);
       S.stats.launches += 1;
       S.stats.kernel_seconds += st.kernel_ms * 1e-3;
+      if (st.event_ms > 0) S.stats.event_seconds += st.event_ms * 1e-3;
       if (st.shader_mhz > 0) {
         S.stats.shader_mhz_sum += st.shader_mhz;
         S.stats.shader_mhz_n += 1;

@@ -91,6 +91,8 @@ struct SearchStats {
   uint64_t shader_mhz_n = 0;
   uint64_t device_checked = 0;     // candidates confirmed on the GPU (khb_check)
   double device_check_seconds = 0; // wall time of those khb_check calls
+  double event_seconds = 0;        // summed HIP-event times of the launches (khb_stats.event_ms: dispatch
+                                   // to end, what rocprofv3's kernel trace reports per launch)
 };
 
 struct SearchCallbacks {

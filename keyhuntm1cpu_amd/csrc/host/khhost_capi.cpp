@@ -234,7 +234,7 @@ int khh_session_run_ex(khh_session* s, const uint8_t* targets_xy, int n_targets,
         st.chunks, st.giant_steps, st.candidates, st.degenerate, (uint64_t)(st.kernel_seconds * 1e6), st.launches,
         st.rescans, (uint64_t)(st.busy_seconds * 1e6),
         st.shader_mhz_n ? (uint64_t)(1e3 * st.shader_mhz_sum / st.shader_mhz_n) : 0, st.device_checked,
-        (uint64_t)(st.device_check_seconds * 1e6)};
+        (uint64_t)(st.device_check_seconds * 1e6), (uint64_t)(st.event_seconds * 1e6)};
     memcpy(stats_out, v, sizeof(uint64_t) * (stats_len < KHH_SESSION_STATS ? stats_len : KHH_SESSION_STATS));
   }
   if (rc) set_err(err, errlen, e);

@@ -342,6 +342,7 @@ void launch_times(khb_ctx* c, const Slot& S, khb_stats* st, bool epilogue) {
   st->shader_mhz = clocks ? (float)(100.0 * (double)(p[2] - p[0]) / (double)(p[3] - p[1])) : 0.f;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, S.ev0, S.ev1) != hipSuccess) ms = -1.f;
+  st->event_ms = ms;
   if (epilogue && q[1] > p[1] && ms >= 0.f) {
     const float span = (float)((double)(q[1] - p[1]) * 1e-5);     // 100 MHz ticks -> ms
     if (span < ms) ms = span;

@@ -54,11 +54,11 @@ class CheckOut(C.Structure):       # khb_check_out
 class Stats(C.Structure):
     _fields_ = [("n_cand", C.c_uint32), ("n_degenerate", C.c_uint32), ("giant_steps", C.c_uint64),
                 ("kernel_ms", C.c_float), ("launch_begin_ms", C.c_double), ("launch_end_ms", C.c_double),
-                ("shader_mhz", C.c_float)]
+                ("shader_mhz", C.c_float), ("event_ms", C.c_float)]
 
 
 _libs: dict[str, C.CDLL] = {}
-KHB_ABI_VERSION = 5
+KHB_ABI_VERSION = 6
 
 
 def lib(path: str | None = None) -> C.CDLL:

@@ -13,7 +13,7 @@ _lib = None
 
 
 KHH_ABI_VERSION = 5                 # include/khhost.h
-KHH_SESSION_STATS, KHH_ADDR_STATS = 11, 8
+KHH_SESSION_STATS, KHH_ADDR_STATS = 12, 8
 
 
 class KhhError(RuntimeError):
@@ -261,7 +261,7 @@ class Tables:
 
 
 _STAT_KEYS = ("chunks", "giant_steps", "candidates", "degenerate", "kernel_s", "launches", "rescans", "busy_s",
-              "shader_mhz", "device_checked", "device_check_s")
+              "shader_mhz", "device_checked", "device_check_s", "event_s")
 CHECK_HOST, CHECK_DEVICE, CHECK_AUTO = 0, 1, 2      # include/khhost.h KHH_CHECK_*
 BSGS_MODES = ("sequential", "backward", "both", "random", "dance")     # keyhunt.cpp:227, -B
 
@@ -319,6 +319,7 @@ class Session:
         st["busy_s"] = stats[7] / 1e6
         st["shader_mhz"] = stats[8] / 1e3
         st["device_check_s"] = stats[10] / 1e6
+        st["event_s"] = stats[11] / 1e6
         return res, st
 
     def set_chunk_mode(self, mode: int) -> None:

@@ -80,8 +80,8 @@ def test_abi_versions_match_headers_and_bindings():
 
 
 def test_khb_stats_layout():
-    """khb_stats as the binding reads it (include/khbsgs.h, ABI 4)."""
+    """khb_stats as the binding reads it (include/khbsgs.h, ABI 6: event_ms fills shader_mhz's padding)."""
     from keyhuntm1cpu_amd.khbsgs import Stats
     assert [f for f, _ in Stats._fields_] == ["n_cand", "n_degenerate", "giant_steps", "kernel_ms", "launch_begin_ms",
-                                             "launch_end_ms", "shader_mhz"]
+                                             "launch_end_ms", "shader_mhz", "event_ms"]
     assert C.sizeof(Stats) == 48

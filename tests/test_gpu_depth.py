@@ -213,7 +213,7 @@ def test_lazy_second_slot_under_a_full_residency_launch():
     full-residency launch on slot 0 with the second slot allocated while it runs.  The second slot's counters are
     zeroed on its own stream (a null-stream hipMemset queued behind the running launch zeroed them mid-launch
     and re-walked 6,144 groups: tools/debug/epilogue_diag.py).  Every collect has the submitted walked count, and
-    the execution span (khb_stats.kernel_ms) is positive and no longer than the launch's events."""
+    the execution span (khb_stats.kernel_ms) is positive and no longer than the launch's events (event_ms)."""
     import ctypes as C
     from keyhuntm1cpu_amd.khbsgs import Engine, Cand, Degenerate, Stats
     t = khhost.Tables(None, 1, threads=16)
@@ -237,4 +237,5 @@ def test_lazy_second_slot_under_a_full_residency_launch():
             assert rc == 0 and st.giant_steps == jobs * t.cycles * 1024, (rc, st.giant_steps)
             assert 0 < st.kernel_ms and st.launch_end_ms - st.launch_begin_ms == pytest.approx(st.kernel_ms, abs=1e-3)
             assert 1000 < st.shader_mhz < 3000
+            assert st.event_ms >= st.kernel_ms - 1e-3, (st.event_ms, st.kernel_ms)
     t.close()

@@ -58,9 +58,12 @@ def main() -> None:
             line = json.loads([ln for ln in f if ln.startswith("{")][-1])
         b = line["roofline"].get("kernel_busy_ms_per_step")
         out.update({"bench_kernel_busy_ms_per_step": b, "bench_ms_per_step": line["ms_per_step"],
-                    "bench_kernel_ms_avg": line["roofline"].get("kernel_ms_avg")})
+                    "bench_kernel_ms_avg": line["roofline"].get("kernel_ms_avg"),
+                    "bench_kernel_event_ms_avg": line["roofline"].get("kernel_event_ms_avg")})
         if b:
             out["trace_over_bench_busy"] = round(out["busy_ms_per_step"] / b, 4)
+        if out["bench_kernel_event_ms_avg"]:     # rocprof's per-launch duration against the bench's events
+            out["trace_over_bench_launch"] = round(out["launch_ms_avg"] / out["bench_kernel_event_ms_avg"], 4)
     print(json.dumps(out))
 
 
