@@ -165,6 +165,39 @@ def physical_gpu(torch, local: int) -> str:
         return "device%d" % local
 
 
+PRODUCT_LIB_DIR = os.path.join(REPO, "keyhuntm1cpu_amd", "lib")
+
+
+def check_lib_dir(args):
+    """A line must name the kernel that produced it: KHB_LIB_DIR redirects the libraries to
+    another build (tools/gpu/bench_ab.sh), which is refused unless --variant names it.  Checked before any rank is
+    started or the GPU is touched."""
+    d = os.environ.get("KHB_LIB_DIR")
+    if d and os.path.realpath(d) != os.path.realpath(PRODUCT_LIB_DIR) and not args.variant:
+        raise SystemExit(f"[bench] KHB_LIB_DIR={d} loads a library other than the in-tree product build; pass "
+                         f"--variant NAME for an A/B run of a timing build (the line is then marked with it)")
+
+
+def lib_record(args) -> dict:
+    """config.lib: the loaded libkhbsgs.so (path, sha256 prefix, khb_build_info's words) and libkhhost.so.  A build
+    whose khb_build_info says it is not the product is refused without --variant; with --variant the names must
+    agree."""
+    import hashlib
+    from keyhuntm1cpu_amd import khbsgs, khhost
+    info = khbsgs.build_info()
+    built_as = info.get("variant", "unknown")
+    if args.variant is None and built_as != "product":
+        raise SystemExit(f"[bench] {info['path']} was built as variant {built_as!r}, not the product: pass --variant")
+    if args.variant is not None and built_as not in (args.variant, "unknown"):
+        raise SystemExit(f"[bench] --variant {args.variant} but {info['path']} was built as {built_as!r}")
+    host_path = os.path.realpath(khhost.LIB_PATH)
+    with open(host_path, "rb") as f:
+        host_sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    rel = lambda p: os.path.relpath(p, REPO) if p.startswith(REPO + os.sep) else p   # noqa: E731
+    return {"lib_sha16": info["sha16"], "lib_path": rel(info["path"]), "host_lib_sha16": host_sha,
+            "host_lib_path": rel(host_path), "build": {k: v for k, v in info.items() if k not in ("sha16", "path")}}
+
+
 def init_gloo(dist, rank: int, world: int):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     # gloo's C++ connect messages go to fd 1; keep stdout for the one JSON line (rank 0)
@@ -229,9 +262,13 @@ def main():
                          "(khb_check) or auto (the GPU for batches of more than 4096 candidates)")
     # launcher self-test (tests/test_launch.py): every rank joins the gloo world and rank 0 prints the
     # ranks' view; no GPU is touched.  --launch-check-fail R makes rank R exit with status 3.
+    ap.add_argument("--variant", default=None,
+                    help="an A/B run of the timing build named NAME in KHB_LIB_DIR: required whenever KHB_LIB_DIR points "
+                         "away from the in-tree keyhuntm1cpu_amd/lib, and the line is then marked \"variant\": NAME")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--launch-check-fail", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    check_lib_dir(args)
     if args.workload == "p130" and args.k != 1:
         raise SystemExit("--workload p130 is BASELINE configs[3]: k = 1")
 
@@ -273,8 +310,9 @@ def main():
     from keyhuntm1cpu_amd import khhost
     from keyhuntm1cpu_amd.partition import blocks_fit, fit_batch, rank_range
     host_threads = min(16, os.cpu_count() or 1)
+    lib_rec = lib_record(args)
     if args.workload == "address":
-        return bench_address(args, world, rank, dist, torch)
+        return bench_address(args, world, rank, dist, torch, lib_rec)
     t0 = time.time()
     tables = khhost.Tables(None, args.k, threads=host_threads, gpl=4)
     t_build = time.time() - t0
@@ -518,10 +556,13 @@ def main():
                    "ref_keys_per_s": "%.3e" % (gsps * 2 * tables.m),
                    "candidates": st["candidates"], "found": [hex(r) if r else None for r in res],
                    "level0_gate": not args.no_gate, "check": args.check,
-                   "device_checked": st["device_checked"], "device_check_s": round(st["device_check_s"], 4)},
+                   "device_checked": st["device_checked"], "device_check_s": round(st["device_check_s"], 4),
+                   **lib_rec},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
+    if args.variant:
+        out["variant"] = args.variant
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -574,7 +615,7 @@ def addr_cpu_baseline(text: str, seconds: float, threads: int, search: int):
     return sum(done) / el
 
 
-def bench_address(args, world, rank, dist, torch):
+def bench_address(args, world, rank, dist, torch, lib_rec):
     from keyhuntm1cpu_amd import khhost
     from keyhuntm1cpu_amd.partition import rank_range
     n_seq, chunks = 1 << 32, args.chunks or 8
@@ -663,10 +704,12 @@ def bench_address(args, world, rank, dist, torch):
                    "targets": len(A.table()), "n_seq": hex(n_seq), "chunks_per_step": chunks,
                    "keys_per_step": chunks * n_seq, "parallelism": "range-partition x%d" % world,
                    "table_build_s": round(t_build, 2), "bloom_hits": st["hits"], "found": len(found),
-                   "launches": st["launches"]},
+                   "launches": st["launches"], **lib_rec},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
+    if args.variant:
+        out["variant"] = args.variant
     print(json.dumps(out), flush=True)
     A.close()
     if world > 1:

@@ -37,6 +37,8 @@ extern "C" {
 #define KHB_EBUSY -6      /* a submission is still in flight */
 #define KHB_EINCOMPLETE -7 /* collect: the groups the kernel counted as walked differ from the submitted
                              n_jobs x group_count (a work-item bookkeeping fault; results incomplete) */
+#define KHB_EHANDOFF -8    /* collect: the launch's end-of-launch hand-off (the last wave's copy of the counters
+                             to pinned host memory) did not count every wave; khb_last_handoff has the counts */
 
 #define KHB_GROUP 1024         /* giant steps per group: CPU_GRP_SIZE, keyhunt.cpp:127 */
 #define KHB_GIANT_TABLE 513    /* GSn[0..511] + _2GSn, keyhunt.cpp:1318-1338 */
@@ -44,9 +46,15 @@ extern "C" {
 /* ABI version of this header (entry points, khb_stats and the other structs); bumped whenever one of
  * them changes.  A binding checks khb_abi_version() == the KHB_ABI_VERSION it was written for before
  * any other call (khb_stats gained launch_begin_ms/launch_end_ms/shader_mhz in ABI 3 and 4; ABI 5 added
- * khb_load_check_tables / khb_check; ABI 6 added khb_stats.event_ms). */
-#define KHB_ABI_VERSION 6
+ * khb_load_check_tables / khb_check; ABI 6 added khb_stats.event_ms; ABI 7 added khb_build_info,
+ * khb_set_gate_stage0, KHB_EHANDOFF / khb_last_handoff and the -m address endomorphism). */
+#define KHB_ABI_VERSION 7
 int khb_abi_version(void);
+/* What this library was built as, one line of `key=value` words: abi, arch, variant ("product" for the in-tree
+ * build; tools/build_variant.sh names its timing builds), the kernel's build defines (waves per SIMD, groups per
+ * work item, gate stages, half prefix stream, extra -D flags) and the compiler.  A bench line records it, so a
+ * number can always be traced to the kernel that produced it. */
+const char* khb_build_info(void);
 
 typedef struct khb_ctx khb_ctx;
 
@@ -77,8 +85,9 @@ typedef struct {
                               khb_reset_epoch (or khb_open); end = the submission's end event, begin = end -
                               kernel_ms; -1 if unavailable.  Two submissions in flight */
   double launch_end_ms;    /* overlap, so the union of these intervals is the device-busy time. */
-  float shader_mhz;        /* average shader clock over the launch (s_memtime / s_memrealtime from its first
-                              wave's start to its last wave's exit), 0 if unavailable */
+  float shader_mhz;        /* average shader clock of block 0's first wave over its lifetime (s_memtime /
+                              s_memrealtime at its start and at its exit; s_memtime counts per XCD, so one
+                              wave's own interval is the one that can be timed), 0 if unavailable */
   float event_ms;          /* the submission's HIP-event time, dispatch to end: the launch duration
                               rocprofv3 --kernel-trace reports (>= kernel_ms; with two submissions in flight
                               it includes the wait behind the other slot's launch), -1 if unavailable */
@@ -92,6 +101,8 @@ int khb_open(int device, uint32_t lanes, khb_ctx** out);
 int khb_close(khb_ctx* ctx);
 const char* khb_strerror(int code);
 int khb_last_hip_error(const khb_ctx* ctx);
+/* After KHB_EHANDOFF: the waves the last collected launch's epilogue counted, and the launch's wave total. */
+int khb_last_handoff(const khb_ctx* ctx, uint32_t* waves_seen, uint32_t* waves_total);
 /* The hipStream_t the context launches on (for external HIP events / synchronisation). */
 void* khb_stream(khb_ctx* ctx);
 /* Persistent-grid size of the context in work lanes (one lane = one work item at a time). */
@@ -144,6 +155,16 @@ int khb_load_gate(khb_ctx* ctx, const uint8_t* gate, uint32_t log2_bits, uint32_
  * 2 MiB for a gate of up to 32 MiB (k = 1), 16 MiB for a larger one (k >= 4). */
 #define KHB_GATE_STAGE1_AUTO 1
 int khb_set_gate_stage1(khb_ctx* ctx, uint32_t log2_bytes);
+/* Stage-0 filter for gates loaded after this call, in front of a stage-1 fold: the hi words of the gate's blocks
+ * (probe 1's bit of every member) OR-folded to 2^log2_bytes bytes of 32-bit words (word i = OR of the hi words of
+ * blocks j with j mod (2^log2_bytes / 4) == i).  x tests bit (w1 >> 5) mod 32 of word w0 mod (2^log2_bytes / 4)
+ * and reads its block of the fold only when it is set: one bit per member, so the same candidates.  Built only
+ * with probes >= 2 and a fold larger than the filter.  0 = no stage 0; otherwise log2_bytes in [10, 30], or
+ * KHB_GATE_STAGE0_AUTO (the default): 2 MiB in front of a fold larger than 2 MiB (k >= 4), none otherwise. */
+#define KHB_GATE_STAGE0_AUTO 1
+int khb_set_gate_stage0(khb_ctx* ctx, uint32_t log2_bytes);
+/* The gate stages the loaded gate runs with: bit 2 the gate, bit 1 its stage-1 fold, bit 0 the stage-0 filter. */
+int khb_gate_stages(const khb_ctx* ctx);
 /* GSn[0..511] and _2GSn (keyhunt.cpp:1325-1338), 513 affine points x||y BE. */
 int khb_load_giant_table(khb_ctx* ctx, const uint8_t* gsn_xy_be);
 /* Lane start offsets: offs[m] = (m*groups_per_lane) * _2GSn, m in [0, n) (offs[0] unused: the

@@ -132,6 +132,7 @@ constexpr int kQueueDepth = 2;
 struct khb_ctx {
   int device = -1;
   int last_hip = 0;
+  uint32_t handoff_seen = 0, handoff_total = 0;   // the last collect's epilogue wave count (khb_last_handoff)
   uint32_t lanes = 0;
   uint8_t* d_bloom = nullptr;
   BloomGeom geom{};
@@ -139,6 +140,9 @@ struct khb_ctx {
   uint8_t* d_gate1 = nullptr;          // its stage-1 fold, null = none
   uint32_t gate1_mask = 0;
   uint32_t gate1_log2 = KHB_GATE1;     // khb_set_gate_stage1: fold size for gates loaded later
+  uint32_t* d_gate0 = nullptr;         // the stage-0 filter, null = none
+  uint32_t gate0_mask = 0;
+  uint32_t gate0_log2 = KHB_GATE0;     // khb_set_gate_stage0: filter size for gates loaded later
   uint32_t gate_mask = 0, gate_probes = 0;
   AffPt* d_gsn = nullptr;
   AffPt* d_offs = nullptr;
@@ -300,6 +304,8 @@ ScanArgs make_args(khb_ctx* c, const Slot& S, uint32_t n_jobs, uint32_t group_be
   A.gate_probes = c->gate_probes;
   A.gate1 = c->d_gate1;
   A.gate1_mask = c->gate1_mask;
+  A.gate0 = c->d_gate0;
+  A.gate0_mask = c->gate0_mask;
   A.gsn = c->d_gsn;
   A.offs = c->d_offs;
   A.gofs = c->gpl == 1 ? c->d_offs : c->d_gofs;
@@ -388,7 +394,12 @@ int prepare_host_launch(khb_ctx* c, Slot& S, ScanArgs& A, uint32_t blocks) {
 }
 
 // After the slot's end event: the epilogue's copy is complete iff it counted every wave of the launch.
-bool host_counters_ok(const Slot& S, uint32_t total_waves) { return S.h_counters[3] == total_waves; }
+// The launch epilogue counted every wave (else KHB_EHANDOFF; the counts are kept for khb_last_handoff).
+bool host_counters_ok(khb_ctx* c, const Slot& S) {
+  c->handoff_seen = S.h_counters[3];
+  c->handoff_total = S.total_waves;
+  return S.h_counters[3] == S.total_waves;
+}
 
 int check_scan_args(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t group_begin, uint32_t group_count,
                     bool bsgs = true) {
@@ -431,6 +442,7 @@ const char* khb_strerror(int code) {
     case KHB_ESTATE: return "call order violated (tables not loaded?)";
     case KHB_EBUSY: return "submission in flight";
     case KHB_EINCOMPLETE: return "the device walked a different number of groups than submitted";
+    case KHB_EHANDOFF: return "the launch's end-of-launch hand-off did not count every wave (khb_last_handoff)";
     default: return "unknown error";
   }
 }
@@ -439,6 +451,28 @@ int khb_last_hip_error(const khb_ctx* c) { return c ? c->last_hip : 0; }
 void* khb_stream(khb_ctx* c) { return c ? (void*)c->slot[0].stream : nullptr; }
 uint32_t khb_lanes(const khb_ctx* c) { return c ? c->lanes : 0; }
 int khb_abi_version(void) { return KHB_ABI_VERSION; }
+
+#ifndef KHB_VARIANT
+#define KHB_VARIANT "product"        // tools/build_variant.sh names its timing builds (-DKHB_VARIANT=\"<name>\")
+#endif
+#ifndef KHB_BUILD_DEFINES
+#define KHB_BUILD_DEFINES ""         // the extra -D flags of a tools/build_variant.sh build, comma-separated
+#endif
+#define KHB_STR2(x) #x
+#define KHB_STR(x) KHB_STR2(x)
+const char* khb_build_info(void) {
+  return "abi=" KHB_STR(KHB_ABI_VERSION) " arch=gfx950 variant=" KHB_VARIANT
+         " waves_per_simd=" KHB_STR(KHB_WAVES_PER_SIMD) " addr_waves_per_simd=" KHB_STR(KHB_ADDR_WAVES_PER_SIMD)
+         " batch=" KHB_STR(KHB_BATCH) " gate1=" KHB_STR(KHB_GATE1) " half_stream=" KHB_STR(KHB_HALF_STREAM)
+         " gate0=" KHB_STR(KHB_GATE0) " defines=" KHB_BUILD_DEFINES " compiler=" __clang_version__;
+}
+
+int khb_last_handoff(const khb_ctx* c, uint32_t* waves_seen, uint32_t* waves_total) {
+  if (!c) return KHB_EINVAL;
+  if (waves_seen) *waves_seen = c->handoff_seen;
+  if (waves_total) *waves_total = c->handoff_total;
+  return KHB_OK;
+}
 
 uint32_t khb_groups_per_item(void) { return kBatch; }
 
@@ -537,6 +571,7 @@ int khb_close(khb_ctx* c) {
   hipFree(c->d_bloom);
   hipFree(c->d_gate);
   hipFree(c->d_gate1);
+  hipFree(c->d_gate0);
   hipFree(c->d_gsn);
   hipFree(c->d_offs);
   hipFree(c->d_gofs);
@@ -552,7 +587,8 @@ int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t 
   KHB_TRY(c, hipSetDevice(c->device));
   if (c->d_gate) { hipFree(c->d_gate); c->d_gate = nullptr; }
   if (c->d_gate1) { hipFree(c->d_gate1); c->d_gate1 = nullptr; }
-  c->gate_mask = c->gate1_mask = 0;
+  if (c->d_gate0) { hipFree(c->d_gate0); c->d_gate0 = nullptr; }
+  c->gate_mask = c->gate1_mask = c->gate0_mask = 0;
   if (!gate) return KHB_OK;
   const size_t bytes = (size_t)1 << (log2_bits - 3);
   // one probe: every block's hi word set on the device copy, so the kernels' fixed three-probe test
@@ -582,7 +618,33 @@ int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t 
     KHB_TRY(c, hipMalloc(&c->d_gate1, nb1 * 8));
     KHB_TRY(c, hipMemcpy(c->d_gate1, f.data(), nb1 * 8, hipMemcpyHostToDevice));
     c->gate1_mask = (uint32_t)(nb1 - 1);
+    // KHB_GATE_STAGE0_AUTO: a 2 MiB one-bit-per-member filter in front of a fold larger than 2 MiB (k >= 4, where
+    // the 16 MiB fold is read from the MALL for every x); none at k = 1, whose 2 MiB fold is itself L2-resident.
+    // With one probe every hi word is set (above), so the filter would pass everything: none.
+    const uint32_t z_log2 = c->gate0_log2 != KHB_GATE_STAGE0_AUTO ? c->gate0_log2 : f_log2 > 21 ? 21u : 0u;
+    if (z_log2 && probes >= 2 && (size_t)1 << z_log2 < nb1 * 8) {
+      // stage 0: the hi words of the gate's blocks (probe 1's bit of every member) OR-folded to 2^z_log2 bytes
+      const size_t nw0 = ((size_t)1 << z_log2) / 4;
+      std::vector<uint32_t> z(nw0, 0);
+      for (size_t j = 0; j < nb; ++j) z[j & (nw0 - 1)] |= (uint32_t)(g[j] >> 32);
+      KHB_TRY(c, hipMalloc(&c->d_gate0, nw0 * 4));
+      KHB_TRY(c, hipMemcpy(c->d_gate0, z.data(), nw0 * 4, hipMemcpyHostToDevice));
+      c->gate0_mask = (uint32_t)(nw0 - 1);
+    }
   }
+  return KHB_OK;
+}
+
+int khb_gate_stages(const khb_ctx* c) {
+  if (!c) return KHB_EINVAL;
+  return (c->d_gate ? 4 : 0) | (c->d_gate1 ? 2 : 0) | (c->d_gate0 ? 1 : 0);
+}
+
+int khb_set_gate_stage0(khb_ctx* c, uint32_t log2_bytes) {
+  if (!c || (log2_bytes && log2_bytes != KHB_GATE_STAGE0_AUTO && (log2_bytes < 10 || log2_bytes > 30)))
+    return KHB_EINVAL;
+  if (c->queued) return KHB_EBUSY;
+  c->gate0_log2 = log2_bytes;
   return KHB_OK;
 }
 
@@ -659,7 +721,7 @@ int khb_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_t gro
   const uint32_t blocks = c->lanes / kBlock;
   if ((rc = prepare_host_launch(c, S, A, blocks))) return rc;
   KHB_TRY(c, hipEventRecord(S.ev0, S.stream));
-  launch_bsgs(c->d_gate1 ? kScanG1 : c->d_gate ? kScanG : kScan, blocks, S.stream, A);
+  launch_bsgs(c->d_gate0 ? kScanG2 : c->d_gate1 ? kScanG1 : c->d_gate ? kScanG : kScan, blocks, S.stream, A);
   KHB_TRY(c, hipGetLastError());
   KHB_TRY(c, hipEventRecord(S.ev1, S.stream));
   S.total_waves = A.total_waves;
@@ -678,7 +740,7 @@ int khb_collect(khb_ctx* c, khb_cand* cand, uint32_t cap, khb_degenerate* degen,
   c->head = (c->head + 1) % kQueueDepth;
   c->queued--;
   KHB_TRY(c, hipEventSynchronize(S.ev1));
-  if (!host_counters_ok(S, S.total_waves)) return KHB_EHIP;   // the launch's epilogue did not complete
+  if (!host_counters_ok(c, S)) return KHB_EHANDOFF;   // the launch's epilogue did not complete
   S.counters_zero = true;
   const uint32_t nc = S.h_counters[0], nd = S.h_counters[1];
   uint32_t take = nc < c->cand_cap ? nc : c->cand_cap;
@@ -843,7 +905,7 @@ int khb_addr_collect(khb_ctx* c, khb_addr_hit* hits, uint32_t cap, khb_stats* st
   c->head = (c->head + 1) % kQueueDepth;
   c->queued--;
   KHB_TRY(c, hipEventSynchronize(S.ev1));
-  if (!host_counters_ok(S, S.total_waves)) return KHB_EHIP;   // the launch's epilogue did not complete
+  if (!host_counters_ok(c, S)) return KHB_EHANDOFF;   // the launch's epilogue did not complete
   S.counters_zero = true;
   const uint32_t nh = S.h_counters[0], nd = S.h_counters[1];
   const uint32_t acap = khb_addr_hit_capacity(c);

@@ -31,6 +31,9 @@ struct AffPt {
 #ifndef KHB_GATE1
 #define KHB_GATE1 1               // default stage-1 fold of the level-0 gate: KHB_GATE_STAGE1_AUTO (khbsgs.h)
 #endif
+#ifndef KHB_GATE0
+#define KHB_GATE0 1               // default stage-0 filter in front of the fold: KHB_GATE_STAGE0_AUTO (khbsgs.h)
+#endif
 #ifndef KHB_WAVES_PER_SIMD
 // occupancy target of k_giant_scan (launch bounds).  Round 4: 4 waves/SIMD (128 VGPRs, 262,144 lanes; the walk's
 // hot path has the same 1,171 VALU per step as at 3 waves) ran 3.0 % faster than 3 (168 VGPRs) with two
@@ -44,6 +47,13 @@ constexpr uint32_t kBlock = 256;
 #define KHB_BATCH 8               // -m bsgs groups per work item (scan_batch): two inversions per item
 #endif
 constexpr uint32_t kBatch = KHB_BATCH;
+#ifndef KHB_HALF_STREAM
+// 1: the half prefix stream (walk_group_g_half): the gated scan's forward pass stores only the odd prefixes and the
+// walk rebuilds each even one from its odd neighbour, one extra product per two walk steps for half the HBM stream.
+// Exact (the same products of the same operands in the same order).  DESIGN.md §5.
+#define KHB_HALF_STREAM 0
+#endif
+constexpr bool kHalfStream = KHB_HALF_STREAM != 0;
 
 // Kernel modes (template argument of scan_group / k_giant_scan).
 enum : int {
@@ -55,9 +65,12 @@ enum : int {
   kAddrDump = 5,   // -m address parity: write every x||y
   kBaby = 6,       // baby-step table build: bloom_add of every x into L1/L2/L3 + bPtable records
   kScanG = 7,      // -m bsgs with a level-0 gate (the product path: walk_group_g)
-  kScanG1 = 8,     // kScanG with the gate's stage-1 fold in front (khb_set_gate_stage1; k >= 4)
+  kScanG1 = 8,     // kScanG with the gate's stage-1 fold in front (khb_set_gate_stage1)
+  kScanG2 = 9,     // kScanG1 with the stage-0 filter in front of the fold (khb_set_gate_stage0; k >= 4)
 };
-constexpr bool is_gated(int m) { return m == kScanG || m == kScanG1; }
+constexpr bool is_gated(int m) { return m == kScanG || m == kScanG1 || m == kScanG2; }
+// filter stages in front of the full gate: 0 (kScanG), 1 (the fold, kScanG1), 2 (filter + fold, kScanG2)
+constexpr int gate_stages(int m) { return m == kScanG2 ? 2 : m == kScanG1 ? 1 : 0; }
 constexpr bool is_scan(int m) { return m == kScan || is_gated(m); }
 constexpr bool is_addr(int m) { return m >= kAddrU && m <= kAddrDump; }
 constexpr bool needs_y(int m) { return m == kAddrU || m == kAddrB || m == kAddrDump; }
@@ -131,6 +144,11 @@ struct ScanArgs {
   // the fold = OR of blocks j of the gate with j & gate1_mask == i; null = no stage 1
   const uint8_t* __restrict__ gate1;
   uint32_t gate1_mask;
+  // stage-0 filter (khb_set_gate_stage0): one bit per baby-step x, the gate's hi words (probe 1) OR-folded to
+  // (gate0_mask + 1) 32-bit words, word i = OR of the hi words of the gate's blocks j with j & gate0_mask == i;
+  // null = no stage 0
+  const uint32_t* __restrict__ gate0;
+  uint32_t gate0_mask;
   uint64_t job_keys;                   // baby steps per job
   uint64_t n_items;
   uint32_t n_jobs, group_begin, group_end, gpl, lanes_per_job, stride, cand_cap, degen_cap;
@@ -252,16 +270,29 @@ __device__ __forceinline__ uint2 gate_block(const uint8_t* g, uint32_t mask, con
 
 // kScanG: gate test of one walk step's two x (x2 absent at step 511: has2 = false, uniform).  Both
 // blocks are loaded before either is waited for; survivors (~0.04 % of x) go to the queue.
-template <bool STAGE1>
+// STAGES (gate_stages): 1 tests the stage-1 fold first, 2 tests the stage-0 filter before the fold.  Each stage
+// is a superset of the next, so the queued x are exactly the full gate's survivors in every case.
+template <int STAGES>
 __device__ __forceinline__ void gate_pair(const ScanArgs& A, ProbeQueue& Q, const Fe& x1, uint32_t step1, bool has2,
                                           const Fe& x2, uint32_t step2, uint32_t job) {
   bool h1, h2;
   const uint32_t s2 = gate_s2(A);
   const GateBits b1 = gate_bits(x1.v[1], s2), b2 = gate_bits(x2.v[1], s2);
-  if constexpr (STAGE1) {
-    // stage 1 (L2-resident fold); the full gate's line is fetched only for its survivors
-    const uint2 f1 = gate_block(A.gate1, A.gate1_mask, x1), f2 = gate_block(A.gate1, A.gate1_mask, x2);
-    const bool s1 = gate_block_pass(f1, b1), s2p = has2 && gate_block_pass(f2, b2);
+  if constexpr (STAGES >= 1) {
+    bool s1 = true, s2p = has2;
+    if constexpr (STAGES == 2) {
+      // stage 0 (L2-resident, one bit per member: ~63 % of x pass at k = 4); the fold's line (read from the MALL at
+      // k = 4) is fetched only for its survivors.  No ballot: with ~63 % passing a wave almost never skips.
+      const uint32_t v1 = A.gate0[x1.v[0] & A.gate0_mask], v2 = A.gate0[x2.v[0] & A.gate0_mask];
+      s1 = (int32_t)shl_mod32(v1, b1.a1) < 0;
+      s2p = has2 && (int32_t)shl_mod32(v2, b2.a1) < 0;
+    }
+    // stage 1 (the fold: L2-resident at k = 1); the full gate's line is fetched only for its survivors
+    uint2 f1, f2;                                  // read only where loaded (s1 / s2p)
+    if (STAGES == 1 || s1) f1 = gate_block(A.gate1, A.gate1_mask, x1);
+    if (STAGES == 1 || s2p) f2 = gate_block(A.gate1, A.gate1_mask, x2);
+    s1 = s1 && gate_block_pass(f1, b1);
+    s2p = s2p && gate_block_pass(f2, b2);
     if (__ballot(s1 || s2p) == 0) return;
     uint2 w1, w2;                                  // read only where loaded (s1 / s2p)
     if (s1) w1 = gate_block(A.gate, A.gate_mask, x1);
@@ -565,7 +596,7 @@ __device__ __forceinline__ void walk_group(const ScanArgs& A, ProbeQueue& Q, con
 // each step's two x gate-tested together (gate_pair).  The first step is peeled and the prefix
 // load is unconditional, so the loop body issues the same vector-memory sequence every time and
 // the waitcnt pass waits for exactly the operand it needs.
-template <bool STAGE1>
+template <int STAGES>
 __device__ __forceinline__ void walk_group_g(const ScanArgs& A, ProbeQueue& Q, const AffPt& C, Fe inv,
                                              uint32_t job, uint32_t j, const Fe* scr) {
   const size_t S = A.stride;
@@ -594,7 +625,7 @@ __device__ __forceinline__ void walk_group_g(const ScanArgs& A, ProbeQueue& Q, c
     fm_mul(s, s, idx);
     fm_sqr_add(x1, s, u);
     x_out<kScanG>(A, x1);
-    gate_pair<STAGE1>(A, Q, x1, base, false, x1, 0, job);
+    gate_pair<STAGES>(A, Q, x1, base, false, x1, 0, job);
   }
   for (int i = (int)kHalf - 2; i >= 0; --i) {
     if (i > 0) {
@@ -616,9 +647,88 @@ __device__ __forceinline__ void walk_group_g(const ScanArgs& A, ProbeQueue& Q, c
     fm_mul(s, s, idx);
     fm_sqr_add(x2, s, u);
     x_out<kScanG>(A, x2);
-    gate_pair<STAGE1>(A, Q, x1, base + kHalf - 1 - (uint32_t)i, true, x2, base + kHalf + 1 + (uint32_t)i, job);
+    gate_pair<STAGES>(A, Q, x1, base + kHalf - 1 - (uint32_t)i, true, x2, base + kHalf + 1 + (uint32_t)i, job);
   }
   probe<false>(A, Q, C.x, job, j, kHalf);        // the centre, pts[512]
+}
+
+// The half prefix stream (KHB_HALF_STREAM): walk_group_g over a forward pass that stored only the odd prefixes
+// P_1, P_3, ..., P_509 (P_i = prod_{k<=i} dx_k).  After the peeled step 511 the walk goes in pairs (even i, odd
+// i - 1): the even step needs P_{i-1}, stored, and then loads P_{i-3}; the odd step rebuilds P_{i-2} =
+// P_{i-3} * dx_{i-2} (one extra product per pair).  Same points, same order and bit-identical x: P_{i-2} is the
+// forward pass's own product of the same operands in the same order.  Half the stream's HBM bytes (16 B per
+// giant step instead of 32) for +4.3 % VALU.
+template <int STAGES>
+__device__ __forceinline__ void half_points(const ScanArgs& A, ProbeQueue& Q, const AffPt& C, const Fe& negCx,
+                                            const Fe& negCy, const Fe& idx, int i, uint32_t base, uint32_t job) {
+  const GsnTable gsn{A.gsn};
+  Fe u, s, x1, x2;
+  const AffPt g = gsn.pt(i);
+  fm_add_lazy(u, gsn.nx(i), negCx);             // nu = -(C.x + GSn.x)
+  fm_add_lazy(s, g.y, C.y);
+  fm_mul(s, s, idx);
+  fm_sqr_add(x1, s, u);
+  x_out<kScanG>(A, x1);
+  fm_add_lazy(s, g.y, negCy);
+  fm_mul(s, s, idx);
+  fm_sqr_add(x2, s, u);
+  x_out<kScanG>(A, x2);
+  gate_pair<STAGES>(A, Q, x1, base + kHalf - 1 - (uint32_t)i, true, x2, base + kHalf + 1 + (uint32_t)i, job);
+}
+
+template <int STAGES>
+__device__ __forceinline__ void walk_group_g_half(const ScanArgs& A, ProbeQueue& Q, const AffPt& C, Fe inv,
+                                                  uint32_t job, uint32_t j, const Fe* scr) {
+  const size_t S = A.stride;
+  const GsnTable gsn{A.gsn};
+  const uint32_t base = j * KHB_GROUP;
+  Fe negCx, negCy;
+  {
+    Fe p;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p.v[k] = k == 0 ? KHB_P0 : (k == 1 ? KHB_P1 : 0xFFFFFFFFu);
+    fm_sub(negCx, p, C.x);
+    fm_sub(negCy, p, C.y);
+  }
+  Fe pre = scr_ld(scr + (size_t)(kHalf - 3) * S);          // P_509
+  Fe idx, dx;
+  // odd step 511: pts[0] = C - GSn[511] only
+  {
+    Fe u, s, x1;
+    fm_add_lazy(dx, gsn.x(kHalf - 2), negCx);
+    fm_mul(idx, pre, dx);                                  // P_510 = P_509 * dx_510
+    fm_mul(idx, inv, idx);
+    fm_add_lazy(dx, gsn.x(kHalf - 1), negCx);
+    fm_mul(inv, inv, dx);
+    const AffPt g = gsn.pt(kHalf - 1);
+    fm_add_lazy(u, gsn.nx(kHalf - 1), negCx);
+    fm_add_lazy(s, g.y, C.y);
+    fm_mul(s, s, idx);
+    fm_sqr_add(x1, s, u);
+    x_out<kScanG>(A, x1);
+    gate_pair<STAGES>(A, Q, x1, base, false, x1, 0, job);
+  }
+  // pairs (even i, odd i - 1), i = 510 ... 2; pre = P_{i-1} on entry
+  for (int i = (int)kHalf - 2; i >= 2; i -= 2) {
+    fm_mul(idx, inv, pre);                                 // even step i: P_{i-1} (odd index, stored)
+    if (i > 2) pre = scr_ld(scr + (size_t)(i - 3) * S);    // P_{i-3} for step i - 1 (and i - 2)
+    fm_add_lazy(dx, gsn.x(i), negCx);
+    fm_mul(inv, inv, dx);
+    half_points<STAGES>(A, Q, C, negCx, negCy, idx, i, base, job);
+    // odd step i - 1: P_{i-2} = P_{i-3} * dx_{i-2} (i - 1 = 1: P_0 = dx_0)
+    fm_add_lazy(dx, gsn.x(i - 2), negCx);
+    if (i > 2) {
+      fm_mul(idx, pre, dx);
+      fm_mul(idx, inv, idx);
+    } else {
+      fm_mul(idx, inv, dx);
+    }
+    fm_add_lazy(dx, gsn.x(i - 1), negCx);
+    fm_mul(inv, inv, dx);
+    half_points<STAGES>(A, Q, C, negCx, negCy, idx, i - 1, base, job);
+  }
+  half_points<STAGES>(A, Q, C, negCx, negCy, inv, 0, base, job);     // step 0: idx = inv
+  probe<false>(A, Q, C.x, job, j, kHalf);
 }
 
 // One reference group centred on C, walked on its own (-m address, baby steps): the 513-element
@@ -817,11 +927,11 @@ __device__ __forceinline__ uint32_t scan_batch(const ScanArgs& A, ProbeQueue& Q,
     }
     // dx_i = GSn[i].x - C.x as the lazy sum GSn[i].x + (p - C.x) (congruent; feeds products only)
     fm_add_lazy(a, gsn.x(0), negCx);
-    scr_st(sg, a);
+    if (!(kHalfStream && is_gated(MODE))) scr_st(sg, a);       // P_0 is not stored by the half stream
     for (uint32_t i = 1; i < kHalf - 1; ++i) {
       fm_add_lazy(dx, gsn.x(i), negCx);
       fm_mul(a, a, dx);
-      scr_st(sg + i * S, a);
+      if (!(kHalfStream && is_gated(MODE)) || (i & 1u)) scr_st(sg + i * S, a);
     }
     fm_add_lazy(dx, gsn.x(kHalf - 1), negCx);
     fm_mul(a, a, dx);
@@ -855,8 +965,10 @@ __device__ __forceinline__ uint32_t scan_batch(const ScanArgs& A, ProbeQueue& Q,
     Fe* const sg = scr + (size_t)g * kHalf * S;
     asm volatile("" ::: "memory");
     const AffPt C{sc[2 * g * S], sc[(2 * g + 1) * S]};
-    if constexpr (is_gated(MODE))
-      walk_group_g<MODE == kScanG1>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
+    if constexpr (is_gated(MODE) && kHalfStream)
+      walk_group_g_half<gate_stages(MODE)>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
+    else if constexpr (is_gated(MODE))
+      walk_group_g<gate_stages(MODE)>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
     else
       walk_group<MODE>(A, Q, C, sg[(kHalf - 1) * S], job, g0 + g, sg);
     if (MODE != kDump && ((degen >> g) & 1u)) {
@@ -987,7 +1099,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(MODE)) void k_giant_scan(Sca
 }
 
 // Launchers of the k_giant_scan instances (one translation unit each, see above).
-void launch_bsgs(int mode, uint32_t blocks, hipStream_t stream, const ScanArgs& A);   // kScan, kScanG, kScanG1, kDump
+void launch_bsgs(int mode, uint32_t blocks, hipStream_t stream, const ScanArgs& A);   // kScan, kScanG, kScanG1, kScanG2, kDump
 void launch_addr(int mode, uint32_t blocks, hipStream_t stream, const ScanArgs& A);   // kAddrU, kAddrC, kAddrB, kAddrDump
 void launch_baby(uint32_t blocks, hipStream_t stream, const ScanArgs& A);             // kBaby
 

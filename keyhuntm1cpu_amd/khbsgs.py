@@ -58,7 +58,7 @@ class Stats(C.Structure):
 
 
 _libs: dict[str, C.CDLL] = {}
-KHB_ABI_VERSION = 6
+KHB_ABI_VERSION = 7
 
 
 def lib(path: str | None = None) -> C.CDLL:
@@ -103,6 +103,12 @@ def lib(path: str | None = None) -> C.CDLL:
         L.khb_load_gate.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32]
         if hasattr(L, "khb_set_gate_stage1"):    # absent only in older timing builds (tools/perf_variants.py)
             L.khb_set_gate_stage1.argtypes = [C.c_void_p, C.c_uint32]
+        if hasattr(L, "khb_build_info"):         # ABI 7
+            L.khb_build_info.restype = C.c_char_p
+            L.khb_build_info.argtypes = []
+            L.khb_set_gate_stage0.argtypes = [C.c_void_p, C.c_uint32]
+            L.khb_gate_stages.argtypes = [C.c_void_p]
+            L.khb_last_handoff.argtypes = [C.c_void_p, P(C.c_uint32), P(C.c_uint32)]
         L.khb_load_lane_offsets.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32]
         L.khb_submit.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]
         L.khb_collect.argtypes = [C.c_void_p, P(Cand), C.c_uint32, P(Degenerate), C.c_uint32, P(Stats)]
@@ -125,13 +131,38 @@ def lib(path: str | None = None) -> C.CDLL:
     return _libs[path]
 
 
+KHB_EHANDOFF = -8
+
+
 def _check(rc: int, ctx=None, L: C.CDLL | None = None) -> None:
     if rc != 0:
         L = L or lib()
         msg = L.khb_strerror(rc).decode()
-        if ctx:
+        if ctx and rc == KHB_EHANDOFF and hasattr(L, "khb_last_handoff"):
+            seen, total = C.c_uint32(0), C.c_uint32(0)
+            L.khb_last_handoff(ctx, C.byref(seen), C.byref(total))
+            msg += f" ({seen.value} of {total.value} waves)"
+        elif ctx:
             msg += f" (hipError {L.khb_last_hip_error(ctx)})"
         raise KhbError(f"khbsgs: {msg} [{rc}]")
+
+
+def build_info(path: str | None = None) -> dict:
+    """khb_build_info of the library at `path` (the in-tree build by default) as a dict, plus its path and the
+    first 16 hex digits of its sha256: what a bench line records so that its number names the kernel."""
+    import hashlib
+    path = os.path.realpath(path or LIB_PATH)
+    L = lib(path)
+    info = {}
+    if hasattr(L, "khb_build_info"):
+        for w in L.khb_build_info().decode().split(" compiler=")[0].split():
+            k, _, v = w.partition("=")
+            info[k] = v
+        info["compiler"] = L.khb_build_info().decode().split(" compiler=", 1)[-1]
+    with open(path, "rb") as f:
+        info["sha16"] = hashlib.sha256(f.read()).hexdigest()[:16]
+    info["path"] = path
+    return info
 
 
 def groups_per_item() -> int:
@@ -197,6 +228,14 @@ class Engine:
         if gate is not None:
             assert len(gate) == (1 << log2_bits) // 8
         _check(self.L.khb_load_gate(self.h, gate, log2_bits if gate is not None else 0, probes), self.h, self.L)
+
+    def set_gate_stage0(self, log2_bytes: int) -> None:
+        """Stage-0 filter size for gates loaded later (0 none, 1 = KHB_GATE_STAGE0_AUTO, else log2 bytes)."""
+        _check(self.L.khb_set_gate_stage0(self.h, log2_bytes), self.h, self.L)
+
+    def gate_stages(self) -> int:
+        """khb_gate_stages: bit 2 gate, bit 1 stage-1 fold, bit 0 stage-0 filter."""
+        return int(self.L.khb_gate_stages(self.h))
 
     def set_gate_stage1(self, log2_bytes: int) -> None:
         """Stage-1 fold size (2^log2_bytes bytes) for gates loaded afterwards; 0 = none."""

@@ -80,9 +80,10 @@ def spawn_ranks(world: int, cmd: Sequence[str], env: Mapping[str, str] | None = 
     """Run `cmd` as `world` rank processes; rank 0's stdout is forwarded to ours, the other ranks' stdout
     goes to our stderr (stdout keeps exactly rank 0's JSON line).  When a rank fails, the others are
     terminated (SIGTERM, then SIGKILL after grace_s) and its exit status is returned; 0 when all succeed.
-    Once any rank has exited, the others have straggler_s to follow (the ranks meet in a final barrier, so a
-    rank still running then is stuck); with timeout_s the whole run has that long.  Either limit stops the
-    remaining ranks the same way and returns 124, as timeout(1) does."""
+    Once rank 0 has exited cleanly, the others have straggler_s to follow (rank 0 is the last to need them:
+    bench.py's other ranks return after the final all_gather and rank 0 alone goes on to the CPU baseline, so
+    only a rank still running after rank 0 is stuck); with timeout_s the whole run has that long.
+    Either limit stops the remaining ranks the same way and returns 124, as timeout(1) does."""
     base = dict(os.environ if env is None else env)
     port = free_port()
     procs: list[subprocess.Popen] = []
@@ -104,7 +105,7 @@ def spawn_ranks(world: int, cmd: Sequence[str], env: Mapping[str, str] | None = 
             pumps.append(t)
         live = set(range(world))
         t_start = time.time()
-        first_exit = None
+        first_exit = None                          # when rank 0 exited cleanly
 
         def stop_live():
             for q in live:
@@ -124,8 +125,8 @@ def spawn_ranks(world: int, cmd: Sequence[str], env: Mapping[str, str] | None = 
                 if c is None:
                     continue
                 live.discard(r)
-                if first_exit is None:
-                    first_exit = time.time()
+                if first_exit is None and r == 0 and c == 0:
+                    first_exit = time.time()      # the straggler clock: rank 0 done, the others should be too
                 if c != 0 and rc == 0:
                     rc = c if c > 0 else 128 - c          # a signal -s reads as 128 + s, like a shell
                     print(f"[bench] rank {r} exited with status {c}; stopping the other ranks",

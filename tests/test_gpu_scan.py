@@ -105,6 +105,44 @@ def test_probe_matches_oracle(eng, bs32, ora):
     assert all(hits[:2000])
 
 
+@pytest.mark.parametrize("geom", ["k1", "k4"])
+def test_probe_reproduces_bloom_bits_fixture(eng, geom):
+    """khb_probe against tests/golden/bloom_bits.json (Python xxhash, not the oracle):
+    256 sub-blooms of the k=1 / k=4 level-1 geometry hold exactly the fixture's bit positions of the
+    first half of its x, each in sub-bloom x[0] (keyhunt.cpp:3948).  The probe of every fixture x must
+    answer 1 iff all 20 of its bits are set there, a fact read off the fixture alone."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "bloom_bits.json")) as f:
+        doc = json.load(f)
+    g = doc["geometries"][geom]
+    nbits, hashes = g["bits"], g["hashes"]
+    nbytes = (nbits + 7) // 8
+    recs = doc["records"]
+    half = len(recs) // 2
+    bf = bytearray(256 * nbytes)
+    sets = [set() for _ in range(256)]
+    for r in recs[:half]:
+        sub = int(r["x"][:2], 16)
+        for v in r[geom]:
+            bf[sub * nbytes + (v >> 3)] |= 1 << (v & 7)
+            sets[sub].add(v)
+    eng.load_bloom(bytes(bf), nbytes, nbits, hashes)
+    xs = b"".join(bytes.fromhex(r["x"]) for r in recs)
+    hits = eng.probe(xs)
+    exp = [1 if all(v in sets[int(r["x"][:2], 16)] for v in r[geom]) else 0 for r in recs]
+    assert list(hits) == exp
+    assert all(hits[:half])
+    # every bit matters: clearing one bit of an inserted x (not shared with another) turns its probe off
+    r = recs[0]
+    sub = int(r["x"][:2], 16)
+    v = r[geom][7]
+    if sum(v in rr[geom] for rr in recs[:half] if int(rr["x"][:2], 16) == sub) == 1:
+        bf[sub * nbytes + (v >> 3)] &= ~(1 << (v & 7)) & 0xFF
+        eng.load_bloom(bytes(bf), nbytes, nbits, hashes)
+        assert eng.probe(bytes.fromhex(r["x"]))[0] == 0
+
+
 @pytest.mark.parametrize("gpl", [1, 4])
 def test_dump_x_matches_oracle(eng, bs32, ora, gpl):
     load_tables(eng, bs32, gpl)
@@ -232,18 +270,25 @@ def test_gate_candidates_exact(eng, bs32, ora, probes):
         gate_ref.append(gt)
     try:
         # stage 1 = 12: the 8 KiB gate is also kept folded to 4 KiB and tested there first
-        # (khb_set_gate_stage1); the candidates must not change
-        for use_gate, stage1, ref in ((False, 0, l1_ref), (True, 0, gate_ref), (True, 12, gate_ref)):
+        # (khb_set_gate_stage1); stage 0 = 10: a 1 KiB filter of the gate's hi words in front of that fold
+        # (khb_set_gate_stage0; built for probes >= 2).  The candidates must not change.
+        for use_gate, stage1, stage0, ref in ((False, 0, 0, l1_ref), (True, 0, 0, gate_ref), (True, 12, 0, gate_ref),
+                                              (True, 12, 10, gate_ref)):
             eng.set_gate_stage1(stage1)
+            eng.set_gate_stage0(stage0)
             eng.load_gate(gate if use_gate else None, lg, probes)
+            exp_stages = (4 if use_gate else 0) | (2 if use_gate and stage1 else 0) | \
+                (1 if use_gate and stage0 and probes >= 2 else 0)
+            assert eng.gate_stages() == exp_stages
             got, degen, _ = eng.scan(b"".join(centres), 0, bs32.cycles)
             per_job = [[] for _ in centres]
             for job, a in got:
                 per_job[job].append(a)
-            assert [sorted(x) for x in per_job] == ref, (use_gate, stage1)
+            assert [sorted(x) for x in per_job] == ref, (use_gate, stage1, stage0)
         assert 0.4 < sum(map(len, gate_ref)) / sum(map(len, l1_ref)) < 0.6
         assert sum(map(len, l1_ref)) > 100000
     finally:
         eng.set_gate_stage1(1)                 # KHB_GATE_STAGE1_AUTO, the library default
+        eng.set_gate_stage0(1)                 # KHB_GATE_STAGE0_AUTO
         eng.load_gate(None)
         load_tables(eng, bs32, gpl)

@@ -99,3 +99,27 @@ def test_overall_timeout_stops_ranks():
     code = "import time\ntime.sleep(3600)\n"
     rc = launch.spawn_ranks(2, [sys.executable, "-c", code], env=_clean_env(), grace_s=1.0, timeout_s=2.0)
     assert rc == 124
+
+
+def test_rank0_may_outlive_the_others():
+    """bench.py's rank 0 runs the CPU baseline alone after the other ranks returned: a rank 0 that
+    outlives them by more than straggler_s is not stopped; the launch returns its status and its stdout."""
+    code = ("import os, time, sys\n"
+            "if os.environ['RANK'] == '0':\n"
+            "    time.sleep(4.0)\n"
+            "    print('rank0-line', flush=True)\n")
+    rc = launch.spawn_ranks(2, [sys.executable, "-c", code], env=_clean_env(), grace_s=1.0, straggler_s=1.0)
+    assert rc == 0
+
+
+def test_bench_gpus_8_launch_check():
+    """bench.py --gpus 8 --launch-check: eight gloo ranks spawned by bench.py itself (no GPU touched), the
+    world the driver's N=8 scaling run starts."""
+    r = _bench(["--gpus", "8", "--launch-check"], _clean_env(), timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8
+    assert [v["rank"] for v in d["ranks"]] == list(range(8))
+    assert len({v["pid"] for v in d["ranks"]}) == 8

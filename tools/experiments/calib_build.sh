@@ -14,10 +14,10 @@
 #   addrwalk_patch.py: the -m address kernels without the hashing (count-only: the x/y walk's VALU).
 #   plainscr_patch.py: the prefix-scratch stream with plain loads and stores (the product's are non-temporal).
 #   fold2_patch.py: the stage-1 gate fold tested with two of the three probes (candidates unchanged).
-#   half_patch.py: the half prefix stream (exact; tools/experiments/half_stream.hpp, round 5).
+#   (round 5's half_patch.py is now the build define KHB_HALF_STREAM in scan_kernels.hpp: build_variant.sh half -DKHB_HALF_STREAM=1.)
 #   scrplain_patch.py: scr_patch with plain accesses (the stream cache-resident; scr2plain / scr1plain, round 5).
 #   early_patch.py: the first x's stage-1 fold load issued before the second x is computed (round 5).
-# Usage: tools/experiments/calib_build.sh pad|rm|scr|pair|defer|nonop|block|addrwalk|plainscr|fold2|half|scrplain|early <name> [-DKEY=VAL ...]
+# Usage: tools/experiments/calib_build.sh pad|rm|scr|pair|defer|nonop|block|addrwalk|plainscr|fold2|scrplain|early <name> [-DKEY=VAL ...]
 set -e
 KIND=$1; NAME=$2; shift 2
 S1=keyhuntm1cpu_amd/csrc/device/fe_asm.hpp
