@@ -17,7 +17,8 @@ CXXFLAGS ?= -O3 -std=c++17 -fPIC -march=x86-64-v3 -Wall -Wextra -Wno-unused-func
 DEV_HDRS  := $(wildcard $(CSRC)/device/*.hpp) $(CSRC)/scan_kernels.hpp $(CSRC)/check_kernel.hpp include/khbsgs.h
 # libkhbsgs: the C ABI (khbsgs.hip) + one translation unit per group of k_giant_scan instances, so
 # `make -j` compiles the heavy kernels in parallel
-HIP_SRCS  := $(CSRC)/khbsgs.hip $(CSRC)/k_bsgs.hip $(CSRC)/k_addr.hip $(CSRC)/k_baby.hip $(CSRC)/k_check.hip
+HIP_SRCS  := $(CSRC)/khbsgs.hip $(CSRC)/k_bsgs.hip $(CSRC)/k_addr.hip $(CSRC)/k_addr_e.hip $(CSRC)/k_baby.hip \
+             $(CSRC)/k_check.hip
 HIP_OBJS  := $(patsubst $(CSRC)/%.hip,build/hip/%.o,$(HIP_SRCS))
 HOST_SRCS := $(CSRC)/host/u256.cpp $(CSRC)/host/secp_host.cpp $(CSRC)/host/bloom_host.cpp \
              $(CSRC)/host/bsgs_host.cpp $(CSRC)/host/bsgs_files.cpp $(CSRC)/host/engine.cpp \

@@ -159,8 +159,10 @@ int khb_set_gate_stage1(khb_ctx* ctx, uint32_t log2_bytes);
  * (probe 1's bit of every member) OR-folded to 2^log2_bytes bytes of 32-bit words (word i = OR of the hi words of
  * blocks j with j mod (2^log2_bytes / 4) == i).  x tests bit (w1 >> 5) mod 32 of word w0 mod (2^log2_bytes / 4)
  * and reads its block of the fold only when it is set: one bit per member, so the same candidates.  Built only
- * with probes >= 2 and a fold larger than the filter.  0 = no stage 0; otherwise log2_bytes in [10, 30], or
- * KHB_GATE_STAGE0_AUTO (the default): 2 MiB in front of a fold larger than 2 MiB (k >= 4), none otherwise. */
+ * with probes >= 2 and a fold larger than the filter.  0 (the default) = no stage 0; otherwise log2_bytes in
+ * [10, 30], or KHB_GATE_STAGE0_AUTO: 2 MiB in front of a fold larger than 2 MiB (k >= 4), none otherwise.  The
+ * default is off because the filter measured 4.6 % slower on config C (k = 4): the extra per-x load costs more
+ * memory-pipeline cycles than the fold reads it saves. */
 #define KHB_GATE_STAGE0_AUTO 1
 int khb_set_gate_stage0(khb_ctx* ctx, uint32_t log2_bytes);
 /* The gate stages the loaded gate runs with: bit 2 the gate, bit 1 its stage-1 fold, bit 0 the stage-0 filter. */
@@ -250,7 +252,7 @@ int khb_field_op(khb_ctx* ctx, int op, const uint8_t* a, const uint8_t* b, uint8
 /* Bloom self-test kernel: hit[i] = bloom_check(level-1, x[i]) for 32-byte BE x values. */
 int khb_probe(khb_ctx* ctx, const uint8_t* xs, uint8_t* hit, uint32_t n);
 
-/* ---- -m address / -m rmd160 (keyhunt.cpp:2586-2937, BTC P2PKH, no endomorphism) ----
+/* ---- -m address / -m rmd160 (keyhunt.cpp:2586-2937, BTC P2PKH, with or without -e) ----
  * The same group walk with the table Gn[i] = (i+1)*stride*G, _2Gn = 1024*stride*G loaded through
  * khb_load_giant_table (init_generator, keyhunt.cpp:4386-4399), lane offsets as above.  A job is
  * one claimed chunk; centres[k] = pubkey(chunk_base_k + 512*stride) (keyhunt.cpp:2587-2589), so
@@ -259,16 +261,23 @@ typedef struct {
   uint32_t job;
   uint32_t group;
   uint32_t t;
-  uint32_t kind;     /* 0 = compressed prefix 02, 1 = compressed prefix 03, 2 = uncompressed */
+  uint32_t kind;     /* form | e << 2.  form: 0 = compressed prefix 02, 1 = compressed prefix 03, 2 = uncompressed
+                        (x, y), 3 = uncompressed (x, p - y), the negated point (-e only).  e: the point itself (0),
+                        or with -e (beta*x, y) = lambda*P (1) and (beta^2*x, y) = lambda^2*P (2), keyhunt.cpp:2646-2763.
+                        Without -e kind is 0, 1 or 2 as before. */
 } khb_addr_hit;
 
 /* The single target bloom of -m address (bloom over 20-byte hash160 values, initBloomFilter,
  * keyhunt.cpp:6559-6576). */
 int khb_load_addr_bloom(khb_ctx* ctx, const uint8_t* bf, uint64_t bytes, uint64_t bits, uint32_t hashes);
-/* search: 0 = uncompress, 1 = compress, 2 = both (keyhunt.cpp:59-61, -l).  Every point's hash160(s)
- * are probed in the bloom; bloom hits are returned (the host runs searchbinary and the key
- * recovery).  group_begin must be a multiple of groups_per_lane.  Submissions share the context's
- * two slots with khb_submit (two in flight, FIFO collect, a third returns KHB_EBUSY). */
+/* search: 0 = uncompress, 1 = compress, 2 = both (keyhunt.cpp:59-61, -l), optionally OR'ed with
+ * KHB_SEARCH_ENDOMORPHISM (-e, keyhunt.cpp:579-585, 2646-2763): per point also beta*x and beta^2*x (compressed:
+ * 6 hashes per point) and, for uncompressed keys, the negated points (6 hashes per point).  Every point's
+ * hash160(s) are probed in the bloom; bloom hits are returned (the host runs searchbinary and the key
+ * recovery: lambda^e * key, negated as the hit's form says).  group_begin must be a multiple of groups_per_lane.
+ * Submissions share the context's two slots with khb_submit (two in flight, FIFO collect, a third returns
+ * KHB_EBUSY). */
+#define KHB_SEARCH_ENDOMORPHISM 4
 int khb_addr_submit(khb_ctx* ctx, const uint8_t* centres_xy_be, uint32_t n_jobs, uint32_t group_begin,
                     uint32_t group_count, int search);
 /* stats->n_cand = number of bloom hits (may exceed cap); giant_steps = keys scanned. */

@@ -19,7 +19,7 @@ extern "C" {
 
 /* ABI version of this header; bumped whenever a signature, a struct or an output array changes.
  * A binding checks khh_abi_version() == the KHH_ABI_VERSION it was written for before any other call. */
-#define KHH_ABI_VERSION 5
+#define KHH_ABI_VERSION 6
 int khh_abi_version(void);
 
 typedef struct khh_tables khh_tables;
@@ -136,7 +136,8 @@ const uint8_t* khh_addr_table(const khh_addr* a, uint64_t* n);
 const uint8_t* khh_addr_bloom(const khh_addr* a, uint64_t* bytes, uint64_t* bits, uint32_t* hashes);
 void khh_addr_giant_table(const khh_addr* a, uint8_t out[513 * 64]);
 uint32_t khh_addr_lane_offsets(const khh_addr* a, uint8_t* out /* n*64, may be NULL */, uint32_t* gpl);
-/* Sequential (random_chunks = 0) or -R search of [start, end) with search 0/1/2 (-l).  Found keys
+/* Sequential (random_chunks = 0) or -R search of [start, end) with search 0/1/2 (-l), OR'ed with
+ * KHB_SEARCH_ENDOMORPHISM (4, include/khbsgs.h) for -e: the found keys are then lambda^e multiples too.  Found keys
  * (32 B BE each) with compressed flags and rmd160s, in discovery order; *n_found may exceed cap.
  * Discovery order is batch order, and (chunk, key) order inside a batch, except after an overflow: a batch
  * whose bloom hits overflowed khb_addr_hit_capacity is rescanned in parts queued behind the batch already
@@ -157,6 +158,12 @@ int khh_addr_search_ex(const khh_addr* a, const uint8_t start_be[32], const uint
                        uint64_t* stats_out, uint32_t stats_len, char* err, size_t errlen);
 /* Tests: bloom-hit ring capacity of the search's launches (0 = the library default, 2^18). */
 int khh_addr_set_hit_capacity(khh_addr* a, uint32_t cap);
+/* The host confirmation of one GPU bloom hit (khb_addr_hit.kind = form | e << 2) of the point with key key_be:
+ * searchbinary of the hash the kind names, then the reference's key recovery (keyhunt.cpp:2789-2937; lambda^e * key,
+ * negated for the other point of a compressed x or for form 3).  Returns 1 and the key / compressed flag when the
+ * hash is a target, 0 when it is not. */
+int khh_addr_confirm(const khh_addr* a, const uint8_t key_be[32], uint32_t kind, uint8_t out_key_be[32],
+                     int* compressed);
 /* hash160 of a public key (x||y BE) and its P2PKH address (out_addr >= 36 bytes) */
 void khh_hash160(const uint8_t xy[64], int compressed, uint8_t out[20]);
 void khh_rmd_to_address(const uint8_t rmd[20], char* out_addr);

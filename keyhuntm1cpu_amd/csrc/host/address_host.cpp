@@ -298,6 +298,45 @@ std::vector<uint8_t> AddrGen::offs_be() const {
 }
 
 // -------------------------------------------------------------------------------- search
+const U256& endo_lambda(int e) {
+  static const U256 L[2] = {[] { U256 v; U256::from_hex("5363ad4cc05c30e0a5261c028812645a122e22ea20816678df02967c1b23bd72", v); return v; }(),
+                            [] { U256 v; U256::from_hex("ac9c52b33fa3cf1f5ad9e3fd77ed9ba4a880b9fc8ec739c2e0cfc810b51283ce", v); return v; }()};
+  return L[e - 1];
+}
+
+// The hash is recomputed from the key (independently of the GPU's): P = (lambda^e * k)*G has x = beta^e * x(k*G)
+// and the same y.  Compressed forms 0/1: the x-only hit belongs to k' or to n - k' (keyhunt.cpp:2811-2822; with -e
+// the reference decides by the parity of y, 2800-2860, which gives the same key).  Uncompressed form 2 is k' itself,
+// form 3 (-e only) the negated point, n - k' (keyhunt.cpp:2876-2920).
+bool confirm_hit(const AddrTargets& T, const U256& key, uint32_t kind, AddrFound* out) {
+  const uint32_t form = kind & 3u, e = kind >> 2;
+  if (e > 2) return false;
+  U256 k;
+  U256::divmod(key, secp_order(), nullptr, &k);
+  if (e) k = mulmod(k, endo_lambda((int)e), secp_order());
+  if (k.is_zero()) return false;
+  const Pt P = mul_g(k);
+  uint8_t h[20];
+  if (form < 2) {
+    hash160_x((uint8_t)(2 + form), P, h);
+    if (!T.searchbinary(h)) return false;
+    uint8_t hc[20];
+    hash160_pub(P, true, hc);
+    out->key = memcmp(h, hc, 20) != 0 ? secp_order() - k : k;
+    out->compressed = true;
+  } else {
+    hash160_pub(form == 2 ? P : negation(P), false, h);
+    if (!T.searchbinary(h)) return false;
+    out->key = form == 2 ? k : secp_order() - k;
+    out->compressed = false;
+  }
+  // without -e the reported key is the scanned key itself (key, not key mod n), as the reference's keyfound
+  if (!e && form == 2) out->key = key;
+  else if (!e && form < 2 && out->key == k) out->key = key;
+  memcpy(out->rmd.data(), h, 20);
+  return true;
+}
+
 namespace {
 
 struct AddrShared {
@@ -313,30 +352,6 @@ struct AddrShared {
   int rc = 0;
 };
 
-// Confirm one GPU bloom hit on the host: searchbinary, then the reference's key recovery.
-bool confirm_hit(const AddrTargets& T, const U256& key, uint32_t kind, AddrFound* out) {
-  U256 k;
-  U256::divmod(key, secp_order(), nullptr, &k);
-  if (k.is_zero()) return false;
-  const Pt P = mul_g(k);
-  uint8_t h[20];
-  if (kind < 2) {
-    hash160_x((uint8_t)(2 + kind), P, h);
-    if (!T.searchbinary(h)) return false;
-    uint8_t hc[20];
-    hash160_pub(P, true, hc);
-    // keyhunt.cpp:2811-2822: the x-only hit belongs to k or to n - k
-    out->key = memcmp(h, hc, 20) != 0 ? secp_order() - key : key;
-    out->compressed = true;
-  } else {
-    hash160_pub(P, false, h);
-    if (!T.searchbinary(h)) return false;
-    out->key = key;
-    out->compressed = false;
-  }
-  memcpy(out->rmd.data(), h, 20);
-  return true;
-}
 
 void device_loop(AddrShared& S, int device) {
   khb_ctx* ctx = nullptr;
@@ -440,7 +455,8 @@ void device_loop(AddrShared& S, int device) {
   };
   auto submit = [&](ABatch& b) {
     return khb_addr_submit(ctx, b.centres.data(), (uint32_t)b.bases.size(), b.group_begin,
-                           b.group_count ? b.group_count : groups, S.cfg.search);
+                           b.group_count ? b.group_count : groups,
+                           S.cfg.search | (S.cfg.endomorphism ? KHB_SEARCH_ENDOMORPHISM : 0));
   };
   // both submission slots up front; on KHB_ENOMEM (large targets or many devices' worth of scratch)
   // one launch at a time instead of failing (advisor r2)

@@ -1,4 +1,4 @@
-// Host side of keyhunt's -m address / -m rmd160 modes (BTC P2PKH, no endomorphism) on libkhbsgs:
+// Host side of keyhunt's -m address / -m rmd160 modes (BTC P2PKH, with or without -e) on libkhbsgs:
 // target loading (forceReadFileAddress, keyhunt.cpp:6300-6358), the generator table
 // (init_generator, keyhunt.cpp:4386-4399), chunk claiming (thread_process, keyhunt.cpp:2546-2567),
 // and the confirmation of GPU bloom hits (searchbinary + key recovery, keyhunt.cpp:2789-2937).
@@ -51,6 +51,7 @@ struct AddrGen {
 
 struct AddrConfig {
   int search = 2;                      // 0 uncompress, 1 compress, 2 both (-l; keyhunt.cpp:59-61, 300)
+  bool endomorphism = false;           // -e (keyhunt.cpp:579-585): beta*x, beta^2*x and negated points
   U256 start{1}, end{1};               // [start, end): n_range_start / n_range_end
   uint64_t n_seq = 1ull << 32;         // keys per claimed chunk (-n, N_SEQUENTIAL_MAX)
   bool random = false;                 // -R: each chunk starts at a random key in [start, end)
@@ -81,6 +82,13 @@ struct AddrCallbacks {
   std::function<bool()> stop;                                  // polled between batches
   std::function<void(const std::string&)> on_warning;          // e.g. the depth-1 fallback
 };
+
+// Confirm one GPU bloom hit (khb_addr_hit.kind = form | e << 2) of the point whose key is `key`: searchbinary of the
+// hash the kind names, then the reference's key recovery (keyhunt.cpp:2789-2937): lambda^e * key, negated when the
+// hit is the other point of the pair.  False when the hash is not a target (a bloom false positive).
+bool confirm_hit(const AddrTargets& T, const U256& key, uint32_t kind, AddrFound* out);
+// lambda and lambda^2 mod n (keyhunt.cpp:582-583)
+const U256& endo_lambda(int e);
 
 // Sequential (or -R random) search over the range; returns 0 or a KHB_E* / -100 code with *err.
 int addr_search(const AddrTargets& T, const AddrGen& G, const AddrConfig& cfg, const AddrCallbacks& cb,

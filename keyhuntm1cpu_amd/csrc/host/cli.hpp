@@ -16,6 +16,7 @@ std::string speed_line(const U256& total, uint64_t seconds);
 struct AddressCli {
   int mode = 1;                       // 1 address, 3 rmd160 (keyhunt.cpp:51-57)
   int search = 2;                     // -l (keyhunt.cpp:300: both)
+  bool endomorphism = false;          // -e (keyhunt.cpp:579-585)
   bool crypto_set = false;            // -c given
   const char* stride = nullptr;       // -I
   bool random = false;                // -R

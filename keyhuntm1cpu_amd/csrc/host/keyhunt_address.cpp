@@ -98,6 +98,7 @@ int run_address_mode(const AddressCli& o) {
   G.build(stride, (uint32_t)(n_seq / 1024), gpl, o.threads > 0 ? o.threads : 1);
   AddrConfig cfg;
   cfg.search = o.search;
+  cfg.endomorphism = o.endomorphism;
   cfg.start = start;
   cfg.end = end;
   cfg.n_seq = n_seq;
@@ -122,7 +123,8 @@ int run_address_mode(const AddressCli& o) {
     printf("\rBase key: %s     \r", base.hex().c_str());
     fflush(stdout);
   };
-  // stats line every -s seconds (keyhunt.cpp:2145-2252): keys = groups * 1024, x2 for -l compress
+  // stats line every -s seconds (keyhunt.cpp:2145-2252): keys = groups * 1024, x6 with -e (keyhunt.cpp:2175-2180:
+  // every -l mode), else x2 for -l compress
   std::thread stat_th([&] {
     const auto t0 = std::chrono::steady_clock::now();
     uint64_t sec = 0;
@@ -134,7 +136,8 @@ int run_address_mode(const AddressCli& o) {
       sec = s;
       if (o.out_seconds && s % o.out_seconds == 0) {
         U256 total(keys_done.load());
-        if (o.search == 1) total = total * 2u;
+        if (o.endomorphism) total = total * 6u;
+        else if (o.search == 1) total = total * 2u;
         std::lock_guard<std::mutex> lk(out_mu);
         printf("\r%s\r", speed_line(total, s).c_str());
         fflush(stdout);

@@ -296,10 +296,7 @@ int main(int argc, char** argv) {
       fprintf(stderr, "[E] keyhunt_amd searches BTC P2PKH addresses only (-c eth is not available)\n");
       exit(EXIT_FAILURE);
     }
-    if (endomorphism) {
-      fprintf(stderr, "[E] keyhunt_amd does not implement -e (endomorphism) for -m %s\n", kModes[mode]);
-      exit(EXIT_FAILURE);
-    }
+    ao.endomorphism = endomorphism;   // keyhunt.cpp:2646-2937 (BTC)
     ao.mode = mode;
     ao.random = bsgs_mode == 3;
     ao.quiet = quiet;

@@ -382,9 +382,12 @@ int khh_addr_search_ex(const khh_addr* a, const uint8_t start_be[32], const uint
                        int random_chunks, const int* devices, int n_devices, uint32_t lanes, uint64_t max_chunks,
                        uint8_t* keys_be, uint8_t* compressed, uint8_t* rmd, uint32_t cap, uint32_t* n_found,
                        uint64_t* stats_out, uint32_t stats_len, char* err, size_t errlen) {
+  const bool endo = search >= 0 && (search & KHB_SEARCH_ENDOMORPHISM);
+  if (endo) search &= ~KHB_SEARCH_ENDOMORPHISM;
   if (!a || !start_be || !end_be || search < 0 || search > 2) return KHB_EINVAL;
   AddrConfig cfg;
   cfg.search = search;
+  cfg.endomorphism = endo;
   cfg.start = U256::from_be(start_be);
   cfg.end = U256::from_be(end_be);
   cfg.n_seq = a->n_seq;
@@ -424,6 +427,16 @@ int khh_addr_set_hit_capacity(khh_addr* a, uint32_t cap) {
   if (!a) return KHB_EINVAL;
   a->hit_cap = cap;
   return KHB_OK;
+}
+
+int khh_addr_confirm(const khh_addr* a, const uint8_t key_be[32], uint32_t kind, uint8_t out_key_be[32],
+                     int* compressed) {
+  if (!a || !key_be) return KHB_EINVAL;
+  AddrFound f;
+  if (!confirm_hit(a->T, U256::from_be(key_be), kind, &f)) return 0;
+  if (out_key_be) f.key.to_be(out_key_be);
+  if (compressed) *compressed = f.compressed ? 1 : 0;
+  return 1;
 }
 
 void khh_hash160(const uint8_t xy[64], int compressed, uint8_t out[20]) {

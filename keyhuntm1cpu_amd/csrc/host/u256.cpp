@@ -184,4 +184,18 @@ U256 random_in(const U256& lo, const U256& hi) {
   return lo + r;
 }
 
+U256 mulmod(const U256& a0, const U256& b, const U256& m) {
+  U256 a, acc;
+  U256::divmod(a0, m, nullptr, &a);
+  for (int i = 255; i >= 0; --i) {
+    uint64_t c = U256::add(acc, acc, acc);
+    if (c || acc >= m) U256::sub(acc, acc, m);
+    if (b.bit(i)) {
+      c = U256::add(acc, acc, a);
+      if (c || acc >= m) U256::sub(acc, acc, m);
+    }
+  }
+  return acc;
+}
+
 }  // namespace khb

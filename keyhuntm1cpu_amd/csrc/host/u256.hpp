@@ -46,6 +46,9 @@ struct U256 {
   static U256 from_be(const uint8_t in[32]);
 };
 
+// a * b mod m (m != 0; a, b any): shift-and-add, for the rare key recoveries (keyhunt's ModMulK1order, -e).
+U256 mulmod(const U256& a, const U256& b, const U256& m);
+
 // Uniform random value in [lo, hi) from getrandom (Int::Rand, Int.cpp:751-765 / Random.cpp:133-145:
 // the -R / -B random policies, non-deterministic like the reference's).
 U256 random_in(const U256& lo, const U256& hi);

@@ -618,9 +618,10 @@ int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t 
     KHB_TRY(c, hipMalloc(&c->d_gate1, nb1 * 8));
     KHB_TRY(c, hipMemcpy(c->d_gate1, f.data(), nb1 * 8, hipMemcpyHostToDevice));
     c->gate1_mask = (uint32_t)(nb1 - 1);
-    // KHB_GATE_STAGE0_AUTO: a 2 MiB one-bit-per-member filter in front of a fold larger than 2 MiB (k >= 4, where
-    // the 16 MiB fold is read from the MALL for every x); none at k = 1, whose 2 MiB fold is itself L2-resident.
-    // With one probe every hi word is set (above), so the filter would pass everything: none.
+    // stage 0 (off by default, KHB_GATE0): KHB_GATE_STAGE0_AUTO puts a 2 MiB one-bit-per-member filter in front of a
+    // fold larger than 2 MiB (k >= 4, where the 16 MiB fold is read from the MALL for every x); none at k = 1, whose
+    // 2 MiB fold is itself L2-resident.  With one probe every hi word is set (above), so the filter would pass
+    // everything: none.
     const uint32_t z_log2 = c->gate0_log2 != KHB_GATE_STAGE0_AUTO ? c->gate0_log2 : f_log2 > 21 ? 21u : 0u;
     if (z_log2 && probes >= 2 && (size_t)1 << z_log2 < nb1 * 8) {
       // stage 0: the hi words of the gate's blocks (probe 1's bit of every member) OR-folded to 2^z_log2 bytes
@@ -867,6 +868,8 @@ int khb_addr_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_
                     int search) {
   int rc = check_scan_args(c, centres, n_jobs, group_begin, group_count, false);
   if (rc) return rc;
+  const bool endo = search >= 0 && (search & KHB_SEARCH_ENDOMORPHISM);
+  if (endo) search &= ~KHB_SEARCH_ENDOMORPHISM;
   if (search < 0 || search > 2) return KHB_EINVAL;
   if (!c->d_abloom) return KHB_ESTATE;
   if (c->queued && c->slot[c->head].kind != 2) return KHB_EBUSY;     // an -m bsgs scan is in flight
@@ -886,7 +889,10 @@ int khb_addr_submit(khb_ctx* c, const uint8_t* centres, uint32_t n_jobs, uint32_
   const uint32_t blocks = c->lanes / kBlock;
   if ((rc = prepare_host_launch(c, S, A, blocks))) return rc;
   KHB_TRY(c, hipEventRecord(S.ev0, S.stream));
-  launch_addr(search == 0 ? kAddrU : search == 1 ? kAddrC : kAddrB, blocks, S.stream, A);
+  if (endo)
+    launch_addr_e(search == 0 ? kAddrUE : search == 1 ? kAddrCE : kAddrBE, blocks, S.stream, A);
+  else
+    launch_addr(search == 0 ? kAddrU : search == 1 ? kAddrC : kAddrB, blocks, S.stream, A);
   KHB_TRY(c, hipGetLastError());
   KHB_TRY(c, hipEventRecord(S.ev1, S.stream));
   S.total_waves = A.total_waves;

@@ -32,7 +32,11 @@ struct AffPt {
 #define KHB_GATE1 1               // default stage-1 fold of the level-0 gate: KHB_GATE_STAGE1_AUTO (khbsgs.h)
 #endif
 #ifndef KHB_GATE0
-#define KHB_GATE0 1               // default stage-0 filter in front of the fold: KHB_GATE_STAGE0_AUTO (khbsgs.h)
+// default stage-0 filter in front of the fold (khb_set_gate_stage0): none.  The 2 MiB filter at k = 4 (KHB_GATE_STAGE0_AUTO)
+// ran 4.6 % SLOWER on config C (48,629 vs 50,948 Mkeys/s, 3 + 3 alternating runs, profiles/r06a/gate0): it cuts the
+// fold's MALL reads to 63 % but adds one L2 lane-load per x, and a gate lane-load costs its memory-pipeline cycles
+// wherever it is served.
+#define KHB_GATE0 0
 #endif
 #ifndef KHB_WAVES_PER_SIMD
 // occupancy target of k_giant_scan (launch bounds).  Round 4: 4 waves/SIMD (128 VGPRs, 262,144 lanes; the walk's
@@ -48,10 +52,13 @@ constexpr uint32_t kBlock = 256;
 #endif
 constexpr uint32_t kBatch = KHB_BATCH;
 #ifndef KHB_HALF_STREAM
-// 1: the half prefix stream (walk_group_g_half): the gated scan's forward pass stores only the odd prefixes and the
-// walk rebuilds each even one from its odd neighbour, one extra product per two walk steps for half the HBM stream.
-// Exact (the same products of the same operands in the same order).  DESIGN.md §5.
-#define KHB_HALF_STREAM 0
+// 1 (the product since round 6): the half prefix stream (walk_group_g_half): the gated scan's forward pass stores only
+// the odd prefixes and the walk rebuilds each even one from its odd neighbour, one extra product per two walk steps
+// for half the HBM stream.  Exact (the same products of the same operands in the same order).  Whole-bench +1.1 % on
+// one box (round 5, profiles/r05e) and +1.2 % on another (55,423 vs 54,777 Mkeys/s, 3 + 3 alternating runs,
+// profiles/r06a/half); the board runs at its power cap and the halved stream lowers the energy per cycle (launch
+// clock 2,310 vs 2,184 MHz).  DESIGN.md §5.
+#define KHB_HALF_STREAM 1
 #endif
 constexpr bool kHalfStream = KHB_HALF_STREAM != 0;
 
@@ -67,13 +74,19 @@ enum : int {
   kScanG = 7,      // -m bsgs with a level-0 gate (the product path: walk_group_g)
   kScanG1 = 8,     // kScanG with the gate's stage-1 fold in front (khb_set_gate_stage1)
   kScanG2 = 9,     // kScanG1 with the stage-0 filter in front of the fold (khb_set_gate_stage0; k >= 4)
+  kAddrUE = 10,    // kAddrU / kAddrC / kAddrB with -e (KHB_SEARCH_ENDOMORPHISM: beta*x, beta^2*x, negated y;
+  kAddrCE = 11,    //   keyhunt.cpp:2646-2763)
+  kAddrBE = 12,
 };
 constexpr bool is_gated(int m) { return m == kScanG || m == kScanG1 || m == kScanG2; }
 // filter stages in front of the full gate: 0 (kScanG), 1 (the fold, kScanG1), 2 (filter + fold, kScanG2)
 constexpr int gate_stages(int m) { return m == kScanG2 ? 2 : m == kScanG1 ? 1 : 0; }
 constexpr bool is_scan(int m) { return m == kScan || is_gated(m); }
-constexpr bool is_addr(int m) { return m >= kAddrU && m <= kAddrDump; }
-constexpr bool needs_y(int m) { return m == kAddrU || m == kAddrB || m == kAddrDump; }
+constexpr bool is_endo(int m) { return m >= kAddrUE && m <= kAddrBE; }
+constexpr bool is_addr(int m) { return (m >= kAddrU && m <= kAddrDump) || is_endo(m); }
+constexpr bool needs_y(int m) { return m == kAddrU || m == kAddrB || m == kAddrDump || m == kAddrUE || m == kAddrBE; }
+constexpr bool addr_compressed(int m) { return m == kAddrC || m == kAddrB || m == kAddrCE || m == kAddrBE; }
+constexpr bool addr_uncompressed(int m) { return m == kAddrU || m == kAddrB || m == kAddrUE || m == kAddrBE; }
 constexpr bool is_dump(int m) { return m == kDump || m == kAddrDump || m == kBaby; }
 #ifndef KHB_ADDR_WAVES_PER_SIMD
 #define KHB_ADDR_WAVES_PER_SIMD KHB_WAVES_PER_SIMD   // occupancy target of the -m address hash kernels
@@ -395,16 +408,60 @@ __device__ __forceinline__ void addr_point(const ScanArgs& A, const Fe& x, const
         o[0] = job; o[1] = j; o[2] = t; o[3] = kind;
       }
     };
-    if constexpr (MODE == kAddrC || MODE == kAddrB) {
-#pragma unroll 1
-      for (uint32_t pre = 2; pre <= 3; ++pre) {
-        hash160_compressed(h, pre, x);
-        if (bloom_check20(A.bloom, A.geom, h)) emit(pre - 2);
+    if constexpr (is_endo(MODE)) {
+      // -e (keyhunt.cpp:2646-2763): lambda*P = (beta*x, y) and lambda^2*P = (beta^2*x, y) (keyhunt.cpp:582-585).
+      // Compressed: the 02 and 03 hashes of x, beta*x, beta^2*x (kinds 0|e<<2, 1|e<<2); uncompressed: (x_e, y) and
+      // (x_e, p - y), the negated point (kinds 2|e<<2, 3|e<<2).  Every x_e is canonical before it is hashed.
+      // beta (keyhunt.cpp:584); beta^2*x is computed as beta*(beta*x), the same canonical value as the reference's
+      // ModMulK1(x, beta2) (beta2 = beta^2 mod p, keyhunt.cpp:585), with one constant and no indexed table
+      const Fe kBeta = {{0x719501eeu, 0xc1396c28u, 0x12f58995u, 0x9cf04975u, 0xac3434e9u, 0x6e64479eu, 0x657c0710u,
+                         0x7ae96a2bu}};
+      Fe ny;
+      if constexpr (addr_uncompressed(MODE)) {
+        Fe p;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p.v[k] = k == 0 ? KHB_P0 : (k == 1 ? KHB_P1 : 0xFFFFFFFFu);
+        fm_sub(ny, p, y);                          // y != 0 on the curve: p - y is canonical
+        fm_canon(ny, ny);
       }
-    }
-    if constexpr (MODE == kAddrU || MODE == kAddrB) {
-      hash160_uncompressed(h, x, y);
-      if (bloom_check20(A.bloom, A.geom, h)) emit(2);
+      Fe xe = x;
+#pragma unroll 1
+      for (uint32_t e = 0; e < 3; ++e) {
+        if (e) {
+          fm_mul(xe, xe, kBeta);
+          fm_canon(xe, xe);
+        }
+        if constexpr (addr_compressed(MODE)) {
+#pragma unroll 1
+          for (uint32_t pre = 2; pre <= 3; ++pre) {
+            hash160_compressed(h, pre, xe);
+            if (bloom_check20(A.bloom, A.geom, h)) emit((pre - 2) | (e << 2));
+          }
+        }
+        if constexpr (addr_uncompressed(MODE)) {
+          // one copy of the two-block hash in the loop body (unrolled twice it spilled ~700 VGPRs)
+#pragma unroll 1
+          for (uint32_t neg = 0; neg < 2; ++neg) {
+            Fe yy;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) yy.v[k] = neg ? ny.v[k] : y.v[k];
+            hash160_uncompressed(h, xe, yy);
+            if (bloom_check20(A.bloom, A.geom, h)) emit((2u + neg) | (e << 2));
+          }
+        }
+      }
+    } else {
+      if constexpr (MODE == kAddrC || MODE == kAddrB) {
+#pragma unroll 1
+        for (uint32_t pre = 2; pre <= 3; ++pre) {
+          hash160_compressed(h, pre, x);
+          if (bloom_check20(A.bloom, A.geom, h)) emit(pre - 2);
+        }
+      }
+      if constexpr (MODE == kAddrU || MODE == kAddrB) {
+        hash160_uncompressed(h, x, y);
+        if (bloom_check20(A.bloom, A.geom, h)) emit(2);
+      }
     }
   }
 }
@@ -1101,6 +1158,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(MODE)) void k_giant_scan(Sca
 // Launchers of the k_giant_scan instances (one translation unit each, see above).
 void launch_bsgs(int mode, uint32_t blocks, hipStream_t stream, const ScanArgs& A);   // kScan, kScanG, kScanG1, kScanG2, kDump
 void launch_addr(int mode, uint32_t blocks, hipStream_t stream, const ScanArgs& A);   // kAddrU, kAddrC, kAddrB, kAddrDump
+void launch_addr_e(int mode, uint32_t blocks, hipStream_t stream, const ScanArgs& A);  // kAddrUE, kAddrCE, kAddrBE
 void launch_baby(uint32_t blocks, hipStream_t stream, const ScanArgs& A);             // kBaby
 
 }  // namespace khbk

@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(LIB_DIR, "libkhhost.so")
 _lib = None
 
 
-KHH_ABI_VERSION = 5                 # include/khhost.h
+KHH_ABI_VERSION = 6                 # include/khhost.h
 KHH_SESSION_STATS, KHH_ADDR_STATS = 12, 8
 
 
@@ -97,6 +97,7 @@ def lib() -> C.CDLL:
                                          C.c_uint32, C.c_uint64, C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint32,
                                          P(C.c_uint32), P(C.c_uint64), C.c_uint32, C.c_char_p, C.c_size_t]
         L.khh_addr_set_hit_capacity.argtypes = [C.c_void_p, C.c_uint32]
+        L.khh_addr_confirm.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_char_p, C.POINTER(C.c_int)]
         L.khh_hash160.argtypes = [C.c_char_p, C.c_int, C.c_char_p]
         L.khh_rmd_to_address.argtypes = [C.c_char_p, C.c_char_p]
         _lib = L
@@ -420,9 +421,20 @@ class Addr:
         if lib().khh_addr_set_hit_capacity(self.h, cap):
             raise KhhError("khh_addr_set_hit_capacity")
 
+    def confirm(self, key: int, kind: int):
+        """khh_addr_confirm: (key, compressed) recovered from a bloom hit of kind `kind` on the point of `key`, or
+        None when its hash is not a target."""
+        out = C.create_string_buffer(32)
+        comp = C.c_int(0)
+        r = lib().khh_addr_confirm(self.h, _b32(key), kind, out, C.byref(comp))
+        if r < 0:
+            raise KhhError(f"khh_addr_confirm [{r}]")
+        return (int.from_bytes(out.raw, "big"), bool(comp.value)) if r == 1 else None
+
     def search(self, start: int, end: int, search: int = 2, devices=(0,), lanes: int = 0, max_chunks: int = 0,
                random_chunks: bool = False, cap: int = 4096):
-        """Found [(key, compressed, rmd160)] in discovery order, plus stats."""
+        """Found [(key, compressed, rmd160)] in discovery order, plus stats.  search | 4 (KHB_SEARCH_ENDOMORPHISM)
+        is -e."""
         keys = C.create_string_buffer(32 * cap)
         comp = C.create_string_buffer(cap)
         rmd = C.create_string_buffer(20 * cap)

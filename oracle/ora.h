@@ -140,6 +140,9 @@ ora_addr_gen* ora_addr_gen_new(const ora_u256* stride);
 void      ora_addr_gen_free(ora_addr_gen* g);
 void      ora_addr_gen_table(const ora_addr_gen* g, uint8_t out[513 * 64]);
 /* one thread_process group (keyhunt.cpp:2586-2711, checks 2789-2937); see ora_addr.c */
+#define ORA_SEARCH_ENDO 4
+void ora_mulmod_n(ora_u256* r, const ora_u256* a, const ora_u256* b);
+void ora_endo_constants(int i, ora_u256* lambda, ora_u256* beta);   /* i = 0: lambda, beta; 1: lambda^2, beta^2 */
 void ora_addr_group(const ora_addr* A, const ora_addr_gen* g, const ora_u256* key, int search, uint8_t* xy,
                     uint32_t* hits, uint32_t hcap, uint32_t* nhits, ora_u256* keys, uint32_t kcap,
                     uint32_t* nkeys);

@@ -128,10 +128,28 @@ def lib() -> C.CDLL:
         L.ora_addr_gen_new.argtypes = [P(U256)]
         L.ora_addr_gen_free.argtypes = [C.c_void_p]
         L.ora_addr_gen_table.argtypes = [C.c_void_p, C.c_char_p]
+        L.ora_mulmod_n.argtypes = [P(U256), P(U256), P(U256)]
+        L.ora_endo_constants.argtypes = [C.c_int, P(U256), P(U256)]
         L.ora_addr_group.argtypes = [C.c_void_p, C.c_void_p, P(U256), C.c_int, C.c_void_p, P(C.c_uint32),
                                      C.c_uint32, P(C.c_uint32), P(U256), C.c_uint32, P(C.c_uint32)]
         _lib = L
     return _lib
+
+
+SEARCH_ENDO = 4
+
+
+def endo_constants(i: int) -> tuple[int, int]:
+    """(lambda, beta) for i = 0, (lambda^2, beta^2) for i = 1 (keyhunt.cpp:582-585)."""
+    lam, beta = U256(), U256()
+    lib().ora_endo_constants(i, C.byref(lam), C.byref(beta))
+    return lam.value(), beta.value()
+
+
+def mulmod_n(a: int, b: int) -> int:
+    r = U256()
+    lib().ora_mulmod_n(C.byref(r), C.byref(U256.of(a)), C.byref(U256.of(b)))
+    return r.value()
 
 
 def xxh64(data: bytes, seed: int) -> int:
@@ -360,13 +378,14 @@ class AddrGen:
         return out.raw
 
     def group(self, A: AddrTable, key: int, search: int = 2, want_xy: bool = False, cap: int = 1 << 12):
-        """One thread_process group at first key `key`: (hits [(t, kind)], keys, xy bytes|None)."""
+        """One thread_process group at first key `key`: (hits [(t, kind)], keys, xy bytes|None).  search | 4 = -e;
+        kind = form | e << 2 (form 0/1 compressed 02/03, 2 uncompressed, 3 uncompressed of -P; e = lambda power)."""
         xy = C.create_string_buffer(1024 * 64) if want_xy else None
         hits = (C.c_uint32 * cap)()
         keys = (U256 * cap)()
         nh, nk = C.c_uint32(0), C.c_uint32(0)
         lib().ora_addr_group(A.h, self.h, C.byref(U256.of(key)), search, xy, hits, cap, C.byref(nh), keys, cap,
                              C.byref(nk))
-        hl = [(int(hits[i]) >> 2, int(hits[i]) & 3) for i in range(min(nh.value, cap))]
+        hl = [(int(hits[i]) >> 4, int(hits[i]) & 15) for i in range(min(nh.value, cap))]
         kl = [keys[i].value() for i in range(min(nk.value, cap))]
         return hl, kl, (xy.raw if want_xy else None)

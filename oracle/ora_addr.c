@@ -9,8 +9,12 @@
  *     base58/base58.c:39-112 (b58tobin) and encoding as :145-189 (b58enc); the bloom sizing of
  *     initBloomFilter keyhunt.cpp:6559-6576; _sort keyhunt.cpp (memcmp order of 20-byte values);
  *   - searchbinary keyhunt.cpp:2311-2335 (literal, including its probe sequence);
- *   - one group of thread_process keyhunt.cpp:2586-2711 and its checks :2789-2937 (no
- *     endomorphism, BTC), the key recovery rules and the chunk claiming of :2546-2567 / :3050-3057.
+ *   - one group of thread_process keyhunt.cpp:2586-2711 and its checks :2789-2937 (BTC), the key
+ *     recovery rules and the chunk claiming of :2546-2567 / :3050-3057; with -e the endomorphism
+ *     points (beta*x, beta^2*x: keyhunt.cpp:579-585, 2646-2676, 2685-2711), their 6 compressed and
+ *     6 uncompressed hashes (2716-2763) and the lambda key recovery (2800-2937).
+ * The -e constants (lambda, lambda^2 mod n; beta, beta^2 mod p) are the reference's literals
+ * (keyhunt.cpp:582-585); tests check lambda*G = (beta*G.x, G.y).
  * Pins: tests/1to32.rmd + tests/1to32.txt (hash160 / address of puzzle keys 1..32), tests/66.rmd,
  * published SHA-256 / RIPEMD-160 test vectors (tests/test_oracle_addr.py).
  */
@@ -388,6 +392,36 @@ static void key_at(ora_u256* r, const ora_u256* base, const ora_u256* stride, ui
   ora_u256_add(r, base, &m);
 }
 
+/* -e constants, keyhunt.cpp:582-585 */
+static const char* LAMBDA_HEX[2] = {"5363ad4cc05c30e0a5261c028812645a122e22ea20816678df02967c1b23bd72",
+                                    "ac9c52b33fa3cf1f5ad9e3fd77ed9ba4a880b9fc8ec739c2e0cfc810b51283ce"};
+static const char* BETA_HEX[2] = {"7ae96a2b657c07106e64479eac3434e99cf0497512f58995c1396c28719501ee",
+                                  "851695d49a83f8ef919bb86153cbcb16630fb68aed0a766a3ec693d68e6afa40"};
+
+/* keyfound.ModMulK1order(&lambda) (IntMod.cpp ModMulK1order): a*b mod n for a, b < 2^256, by shift-and-add */
+static void mulmod_n(ora_u256* r, const ora_u256* a0, const ora_u256* b) {
+  const ora_u256* n = ora_order();
+  ora_u256 a = *a0, acc;
+  while (ora_u256_cmp(&a, n) >= 0) ora_u256_sub(&a, &a, n);
+  ora_u256_set64(&acc, 0);
+  for (int i = 255; i >= 0; --i) {
+    uint64_t c = ora_u256_add(&acc, &acc, &acc);
+    if (c || ora_u256_cmp(&acc, n) >= 0) ora_u256_sub(&acc, &acc, n);
+    if ((b->w[i / 64] >> (i % 64)) & 1) {
+      c = ora_u256_add(&acc, &acc, &a);
+      if (c || ora_u256_cmp(&acc, n) >= 0) ora_u256_sub(&acc, &acc, n);
+    }
+  }
+  *r = acc;
+}
+
+void ora_mulmod_n(ora_u256* r, const ora_u256* a, const ora_u256* b) { mulmod_n(r, a, b); }
+
+void ora_endo_constants(int i, ora_u256* lambda, ora_u256* beta) {
+  if (lambda) ora_u256_from_hex(lambda, LAMBDA_HEX[i]);
+  if (beta) ora_u256_from_hex(beta, BETA_HEX[i]);
+}
+
 static void neg_mod_n(ora_u256* k) {
   /* keyfound.Neg(); keyfound.Add(&order) */
   ora_u256 z;
@@ -398,10 +432,11 @@ static void neg_mod_n(ora_u256* k) {
 
 /* One group of thread_process (keyhunt.cpp:2586-2711 + checks 2789-2937), BTC, no endomorphism.
  * key: the group's first key (key_mpz before the j loop).  search: 0 uncompress, 1 compress,
- * 2 both (keyhunt.cpp:59-61).  xy (nullable) receives the 1024 points x||y BE in t order.
- * hits receive every bloom hit as (t << 2 | kind), kind 0 = 02-prefix, 1 = 03-prefix,
- * 2 = uncompressed; keys/nkeys the keys that also passed searchbinary (after the reference's sign
- * fix-up). */
+ * 2 both (keyhunt.cpp:59-61), plus ORA_SEARCH_ENDO (4) for -e.  xy (nullable) receives the 1024
+ * points x||y BE in t order.  hits receive every bloom hit as (t << 4 | kind): kind = form | e << 2,
+ * form 0 = 02-prefix, 1 = 03-prefix, 2 = uncompressed (x, y), 3 = uncompressed (x, -y) (-e only),
+ * e = 0 for the point itself, 1 for (beta*x, y) = lambda*P, 2 for (beta^2*x, y) = lambda^2*P (-e only).
+ * keys/nkeys the keys that also passed searchbinary (after the reference's sign fix-up). */
 void ora_addr_group(const ora_addr* A, const ora_addr_gen* g, const ora_u256* key, int search, uint8_t* xy,
                     uint32_t* hits, uint32_t hcap, uint32_t* nhits, ora_u256* keys, uint32_t kcap,
                     uint32_t* nkeys) {
@@ -428,6 +463,8 @@ void ora_addr_group(const ora_addr* A, const ora_addr_gen* g, const ora_u256* ke
     dx[k] = nv;
   }
   dx[0] = inverse;
+  const int endo = (search & 4) != 0;
+  search &= 3;
   const int calc_y = search == 0 || search == 2;
   pts[AHALF] = startP;
   for (i = 0; i < AHALF - 1; ++i) {
@@ -478,30 +515,70 @@ void ora_addr_group(const ora_addr* A, const ora_addr_gen* g, const ora_u256* ke
       ora_u256_to_be(&pts[t].x, xy + 64 * t);
       ora_u256_to_be(&pts[t].y, xy + 64 * t + 32);
     }
-  /* checks, keyhunt.cpp:2789-2937: per point, compressed (02, 03) then uncompressed */
+  /* checks, keyhunt.cpp:2789-2937: per point, compressed then uncompressed.  Without -e: 02, 03,
+   * uncompressed.  With -e (2716-2763): l = 0..5 the 02/03 hashes of x, beta*x, beta^2*x (ModMulK1 of x
+   * with beta / beta2, 2663-2676 and 2685-2711 for pts[512] and pts[0]), l = 6..11 the uncompressed
+   * hashes of (x, y), (x, -y), (beta*x, y), (beta*x, -y), (beta^2*x, y), (beta^2*x, -y). */
+  ora_u256 beta[2], lambda[2];
+  for (int e = 0; e < 2; ++e) ora_endo_constants(e, &lambda[e], &beta[e]);
   for (int t = 0; t < AGRP; ++t) {
-    uint8_t h[3][20];
-    int kinds[3], nk = 0;
+    uint8_t h[12][20];
+    int kinds[12], nk = 0;
+    ora_point ep[3];
+    ep[0] = pts[t];
+    if (endo)
+      for (int e = 1; e < 3; ++e) {
+        ora_fe_mulK1(&ep[e].x, &pts[t].x, &beta[e - 1]);
+        ep[e].y = pts[t].y;
+      }
+    const int ne = endo ? 3 : 1;
     if (search == 1 || search == 2) {
-      ora_x_hash160(0x02, &pts[t].x, h[nk]); kinds[nk++] = 0;
-      ora_x_hash160(0x03, &pts[t].x, h[nk]); kinds[nk++] = 1;
+      for (int e = 0; e < ne; ++e) {
+        ora_x_hash160(0x02, &ep[e].x, h[nk]); kinds[nk++] = 0 | (e << 2);
+        ora_x_hash160(0x03, &ep[e].x, h[nk]); kinds[nk++] = 1 | (e << 2);
+      }
     }
     if (search == 0 || search == 2) {
-      ora_pub_hash160(&pts[t], 0, h[nk]); kinds[nk++] = 2;
+      for (int e = 0; e < ne; ++e) {
+        ora_pub_hash160(&ep[e], 0, h[nk]); kinds[nk++] = 2 | (e << 2);
+        if (endo) {
+          ora_point q;
+          ora_negation(&q, &ep[e]);       /* secp->Negation (SECP256K1.cpp) */
+          ora_pub_hash160(&q, 0, h[nk]); kinds[nk++] = 3 | (e << 2);
+        }
+      }
     }
     for (int l = 0; l < nk; ++l) {
       if (!ora_bloom_check(&A->bloom, h[l], 20)) continue;
-      if (*nhits < hcap) hits[*nhits] = ((uint32_t)t << 2) | (uint32_t)kinds[l];
+      if (*nhits < hcap) hits[*nhits] = ((uint32_t)t << 4) | (uint32_t)kinds[l];
       ++*nhits;
       if (!ora_addr_searchbinary(A, h[l])) continue;
       ora_u256 kf;
       key_at(&kf, key, &g->stride, (uint32_t)t);
-      if (kinds[l] < 2) {
-        /* compressed x-only hit: the key or its negation (keyhunt.cpp:2811-2822) */
-        ora_point pub;
-        uint8_t hh[20];
+      const int form = kinds[l] & 3, e = kinds[l] >> 2;
+      ora_point pub;
+      if (!endo) {
+        if (form < 2) {
+          /* compressed x-only hit: the key or its negation (keyhunt.cpp:2811-2822) */
+          uint8_t hh[20];
+          ora_compute_pubkey(&pub, &kf);
+          ora_pub_hash160(&pub, 1, hh);
+          if (memcmp(h[l], hh, 20) != 0) neg_mod_n(&kf);
+        }
+      } else if (form < 2) {
+        /* keyhunt.cpp:2800-2860: the parity of the ORIGINAL key's y (lambda*P has the same y) decides the
+         * sign; for beta / beta^2 hits the key is multiplied by lambda / lambda^2 first */
         ora_compute_pubkey(&pub, &kf);
-        ora_pub_hash160(&pub, 1, hh);
+        if (e) mulmod_n(&kf, &kf, &lambda[e - 1]);
+        const int odd = (int)(pub.y.w[0] & 1);
+        if ((form == 0 && odd) || (form == 1 && !odd)) neg_mod_n(&kf);
+      } else {
+        /* keyhunt.cpp:2876-2920: lambda^e first, then the uncompressed hash of the key's own public key
+         * decides the sign */
+        uint8_t hh[20];
+        if (e) mulmod_n(&kf, &kf, &lambda[e - 1]);
+        ora_compute_pubkey(&pub, &kf);
+        ora_pub_hash160(&pub, 0, hh);
         if (memcmp(h[l], hh, 20) != 0) neg_mod_n(&kf);
       }
       if (*nkeys < kcap) keys[*nkeys] = kf;

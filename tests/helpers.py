@@ -42,3 +42,20 @@ def gate_bits(lg: int, probes: int, x: int) -> list[int]:
 
 def gate_pass(gate: bytes, lg: int, probes: int, x: int) -> bool:
     return all((gate[b >> 3] >> (b & 7)) & 1 for b in gate_bits(lg, probes, x))
+
+
+def endo_planted_text(ora, picks, seed):
+    """Target lines for keys +-lambda^e * k (e = 0, 1, 2), compressed or not, for the keys k in picks; returns the
+    text and the planted keys with their compressed flag."""
+    import random
+    rng = random.Random(seed)
+    lams = [1] + [ora.endo_constants(i)[0] for i in range(2)]
+    lines, planted = [], []
+    for k in picks:
+        e, neg, comp = rng.randrange(3), rng.randrange(2), rng.randrange(2) == 1
+        K = lams[e] * k % ora.ORDER
+        if neg:
+            K = ora.ORDER - K
+        lines.append(ora.pub_hash160(ora.pubkey(K), comp).hex())
+        planted.append((K, comp, e))
+    return "\n".join(lines) + "\n", planted

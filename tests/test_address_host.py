@@ -11,6 +11,7 @@ import random
 import pytest
 
 from keyhuntm1cpu_amd import khhost
+from tests.helpers import endo_planted_text
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
@@ -154,3 +155,69 @@ def test_host_bloom_multiplier_clamped_below_10000(ora):
     assert a1.bloom() == a4.bloom()
     a1.close()
     a4.close()
+
+
+def test_oracle_endomorphism_constants(ora):
+    """-e (keyhunt.cpp:579-585): lambda*P = (beta*x, y) for the reference's literals, checked against scalar
+    multiplication on G and on a random point; lambda^3 = 1 (mod n), beta^3 = 1 (mod p)."""
+    import random
+    N, P = ora.ORDER, ora.P
+    rng = random.Random(3)
+    for i in range(2):
+        lam, beta = ora.endo_constants(i)
+        assert pow(lam, 3, N) == 1 and pow(beta, 3, P) == 1
+        for k in (1, rng.randrange(1, N)):
+            a, b = ora.pubkey(k), ora.pubkey(lam * k % N)
+            assert (b.x.value(), b.y.value()) == (beta * a.x.value() % P, a.y.value())
+    assert ora.endo_constants(1)[0] == pow(ora.endo_constants(0)[0], 2, ora.ORDER)
+    assert ora.endo_constants(1)[1] == pow(ora.endo_constants(0)[1], 2, ora.P)
+
+
+@pytest.mark.parametrize("search", [0, 1, 2])
+def test_oracle_endomorphism_group_recovers_planted_keys(ora, search):
+    """The oracle's -e group loop (ora_addr.c; keyhunt.cpp:2646-2937) recovers exactly the planted keys
+    +-lambda^e * k of its -l mode, each through the reference's sign rule; without -e only e = 0 keys of k
+    itself (or n - k for compressed hashes) come back.  Pins the endomorphism branch against scalar
+    multiplication (ora.pubkey), which the group loop does not use."""
+    import random
+    rng = random.Random(40 + search)
+    base, ngroups = 0x7000000000 + 1, 4
+    picks = rng.sample(range(base, base + 1024 * ngroups), 60)
+    text, planted = endo_planted_text(ora, picks, search)
+    O = ora.AddrTable(text)
+    gen = ora.AddrGen(1)
+    keys_e, keys = [], []
+    for g in range(ngroups):
+        keys_e += gen.group(O, base + 1024 * g, search | ora.SEARCH_ENDO)[1]
+        keys += gen.group(O, base + 1024 * g, search)[1]
+    want = lambda c: (search == 2) or (search == 1 and c) or (search == 0 and not c)   # noqa: E731
+    assert sorted(keys_e) == sorted(K for K, c, _ in planted if want(c))
+    base_only = sorted(K for K, c, e in planted if want(c) and e == 0 and (c or K < ora.ORDER // 2))
+    assert sorted(keys) == base_only
+    assert len(keys_e) > len(keys)
+
+
+@pytest.mark.parametrize("search", [0, 1, 2])
+def test_host_confirm_matches_oracle_endomorphism(ora, search):
+    """The host's confirmation of every bloom hit of the oracle's -e groups (khh_addr_confirm = address_host.cpp
+    confirm_hit: lambda^e * key, the sign of the hit's form) recovers exactly the oracle's keys (keyhunt.cpp:
+    2789-2937), and the plain kinds 0/1/2 still recover the non -e keys."""
+    import random
+    rng = random.Random(50 + search)
+    base, ngroups = 0x7100000000 + 1, 4
+    picks = rng.sample(range(base, base + 1024 * ngroups), 60)
+    text, planted = endo_planted_text(ora, picks, 10 + search)
+    O = ora.AddrTable(text)
+    A = khhost.Addr(text, n_seq=1024 * ngroups)
+    gen = ora.AddrGen(1)
+    for flag in (ora.SEARCH_ENDO, 0):
+        got, ref = [], []
+        for g in range(ngroups):
+            hits, keys, _ = gen.group(O, base + 1024 * g, search | flag)
+            ref += keys
+            for t, kind in hits:
+                r = A.confirm(base + 1024 * g + t, kind)
+                if r is not None:
+                    got.append(r[0])
+                    assert r[1] == ((kind & 3) < 2)
+        assert sorted(got) == sorted(ref) and ref, flag

@@ -293,3 +293,57 @@ def test_addr_random_chunk_mode_finds_the_key(keys):
                          random_chunks=True)
     assert key in [k for k, c, _ in found]
     assert 1 <= st["chunks"] <= 40
+
+
+@pytest.mark.parametrize("search", [0, 1, 2])
+def test_addr_endomorphism_hits_match_oracle(eng, ora, search):
+    """-e (KHB_SEARCH_ENDOMORPHISM; keyhunt.cpp:579-585, 2646-2763, 2789-2937): 48 groups with 1,500 planted targets
+    +-lambda^e * k (e = 0, 1, 2; compressed or uncompressed).  The GPU's bloom-hit set (g, t, kind = form | e << 2)
+    equals the oracle's in every -l mode, and the host search recovers exactly the oracle's keys, which are the
+    planted keys of that mode."""
+    from tests.helpers import endo_planted_text
+    rng = random.Random(60 + search)
+    base, ngroups = 0x4100000000 + 1, 48
+    picks = rng.sample(range(base, base + 1024 * ngroups), 1500)
+    text, planted = endo_planted_text(ora, picks, 70 + search)
+    A = khhost.Addr(text, n_seq=1024 * ngroups, gpl=4)
+    _load(eng, A)
+    O = ora.AddrTable(text)
+    gen = ora.AddrGen(1)
+    ref_hits, ref_keys = _oracle_groups(ora, O, gen, base, ngroups, search | ora.SEARCH_ENDO)
+    hits, st = eng.addr_scan(khhost.pubkey(base + 512), 0, ngroups, search | ora.SEARCH_ENDO)
+    assert st.giant_steps == 1024 * ngroups
+    assert sorted((g, t, kind) for _, g, t, kind in hits) == ref_hits
+    assert {kind >> 2 for _, _, kind in ref_hits} == {0, 1, 2}
+    want = [K for K, c, _ in planted if search == 2 or (search == 1) == c]
+    assert sorted(ref_keys) == sorted(want)
+    found, st2 = A.search(base, base + 1024 * ngroups, search=search | ora.SEARCH_ENDO, lanes=16384)
+    assert sorted(k for k, _, _ in found) == sorted(ref_keys)
+    # without -e the same file yields only the e = 0 keys (the plain kernels are unchanged)
+    hits0, _ = eng.addr_scan(khhost.pubkey(base + 512), 0, ngroups, search)
+    ref0, _ = _oracle_groups(ora, O, gen, base, ngroups, search)
+    assert sorted((g, t, kind) for _, g, t, kind in hits0) == ref0
+
+
+def test_cli_endomorphism_lambda_multiples(tmp_path, keys, ora):
+    """keyhunt_amd -m address -e -l compress: a target file holding the compressed addresses of lambda * k20 and of
+    n - lambda^2 * k21 (puzzles #20 and #21 of tests/1to32.txt, keyhunt.cpp:582-585) is solved over [1, 2^33),
+    each key reported once with the reference's Hit lines, and the stats line counts x6 keys (keyhunt.cpp:2175-2180)."""
+    import re
+    k20, k21 = int(keys["20"]["key"], 16), int(keys["21"]["key"], 16)
+    lam = ora.endo_constants(0)[0]
+    lam2 = ora.endo_constants(1)[0]
+    K1 = lam * k20 % N
+    K2 = N - lam2 * k21 % N
+    text = "\n".join(khhost.rmd_to_address(khhost.hash160(khhost.pubkey(K), True)) for K in (K1, K2)) + "\n"
+    (tmp_path / "endo.txt").write_text(text)
+    n_seq = 1 << 28
+    r = _cli(["-m", "address", "-f", "endo.txt", "-e", "-l", "compress", "-r", "1:200000000", "-n", hex(n_seq),
+              "-q", "-s", "1"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "[+] Endomorphism enabled\n" in r.stdout
+    for K in (K1, K2):
+        assert r.stdout.count(f"Hit! Private Key: {K:x}\n") == 1, K
+    totals = [int(m) for m in re.findall(r"Total (\d+) keys in", r.stdout)]
+    assert totals, r.stdout[-2000:]
+    assert all(t % (6 * n_seq) == 0 and t // 6 <= (1 << 33) for t in totals)

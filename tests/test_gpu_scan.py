@@ -289,6 +289,6 @@ def test_gate_candidates_exact(eng, bs32, ora, probes):
         assert sum(map(len, l1_ref)) > 100000
     finally:
         eng.set_gate_stage1(1)                 # KHB_GATE_STAGE1_AUTO, the library default
-        eng.set_gate_stage0(1)                 # KHB_GATE_STAGE0_AUTO
+        eng.set_gate_stage0(0)                 # the library default: no stage 0
         eng.load_gate(None)
         load_tables(eng, bs32, gpl)

@@ -13,7 +13,7 @@ mkdir -p $OUT $OBJ
 DEFS=$(echo "$*" | tr ' ' ',')
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value $* -DKHB_VARIANT=\"$NAME\" -DKHB_BUILD_DEFINES=\"$DEFS\""
 pids=()
-for s in khbsgs k_bsgs k_addr k_baby k_check; do
+for s in khbsgs k_bsgs k_addr k_addr_e k_baby k_check; do
   /opt/rocm/bin/hipcc $FLAGS -c -o $OBJ/$s.o keyhuntm1cpu_amd/csrc/$s.hip & pids+=($!)
 done
 for p in ${pids[@]}; do wait $p; done
