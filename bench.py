@@ -236,6 +236,8 @@ def main():
                     help="p66: BASELINE configs[1] (-b 66; --k 4 = configs[2]); p130: configs[3] (-b 130); "
                          "address: configs[4] (-m address unsolvedpuzzles.rmd, -l both)")
     ap.add_argument("--search", type=int, default=2, help="--workload address: -l 0 uncompress, 1 compress, 2 both")
+    ap.add_argument("--endo", action="store_true",
+                    help="--workload address: -e (endomorphism: beta*x, beta^2*x and negated points, keyhunt.cpp:2646-2763)")
     # default: >= 30 s of steady state — 100 steps x 2^34 giant steps at ~360 ms
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
@@ -484,8 +486,11 @@ def main():
             with open(pmc_path) as f:
                 pmc = json.load(f)
             # the PMC record applies only to the kernel it was measured on
+            build = lib_rec["build"]
             note = pmc_mismatch(pmc, {"k": args.k, "level0_gate": not args.no_gate, "lanes": lanes,
-                                      "waves_per_simd": waves})
+                                      "waves_per_simd": waves,
+                                      "kernel_build": {k: build.get(k) for k in ("variant", "half_stream", "batch",
+                                                                                 "waves_per_simd", "gate1", "gate0")}})
             if note:
                 roofline["traffic_note"] = note
             else:
@@ -629,14 +634,15 @@ def bench_address(args, world, rank, dist, torch, lib_rec):
     per_rank = (args.warmup + args.steps) * chunks
     if start + per_rank * n_seq > end:
         raise SystemExit("[bench] -b 71 block too small for the requested steps")
+    search = args.search | (4 if args.endo else 0)          # KHB_SEARCH_ENDOMORPHISM
     if args.warmup:
-        A.search(start, start + args.warmup * chunks * n_seq, search=args.search)
+        A.search(start, start + args.warmup * chunks * n_seq, search=search)
     tstart = start + args.warmup * chunks * n_seq
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    found, st = A.search(tstart, tstart + args.steps * chunks * n_seq, search=args.search)
+    found, st = A.search(tstart, tstart + args.steps * chunks * n_seq, search=search)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -665,7 +671,7 @@ def bench_address(args, world, rank, dist, torch, lib_rec):
     roofline = {"bound": "valu", "unit": "T lane-instr/s", "kernel": "k_giant_scan<address>",
                 "time_basis": "wall time of the timed steps (two launches in flight, as the CLI runs them)",
                 "shader_mhz_avg": round(mhz, 1)}
-    e = ADDR_EXEC_VALU_PER_KEY.get(args.search)
+    e = None if args.endo else ADDR_EXEC_VALU_PER_KEY.get(args.search)
     if e and mhz > 0:
         peak = CUS * 4 * 64 / ADDR_MIX_CYCLES_PER_INSTR * mhz * 1e6 / 1e12
         ach = e * per_gpu / 1e12
@@ -675,22 +681,26 @@ def bench_address(args, world, rank, dist, torch, lib_rec):
                                        "full-rate / 57 %% half-rate VALU, profiles/r03_valu_cost.txt) x 1024 SIMDs at "
                                        "the launches' measured shader clock" % ADDR_MIX_CYCLES_PER_INSTR,
                          "executed_source": "profiles/r04b/addr_libkhbsgs (PMC SQ_INSTS_VALU, tools/addr_floor.py)"})
-        fl = ADDR_FLOOR_TERMS.get(args.search)
+        fl = None if args.endo else ADDR_FLOOR_TERMS.get(args.search)
         if fl:
             floor = sum(fl.values())
             roofline.update({"floor_valu_lane_instr_per_key": round(floor, 1), "floor_terms": fl,
                              "executed_over_floor": round(e / floor, 4),
                              "floor_basis": "hash blocks compiled alone (profiles/r02_hash_isa_counts.txt) + the x/y "
                                             "walk's PMC count in the hash-less build (profiles/r04b)"})
-    roofline["algorithmic_ops_per_key"] = ADDR_ALG_OPS[args.search]
+    if not args.endo:
+        roofline["algorithmic_ops_per_key"] = ADDR_ALG_OPS[args.search]
+    else:
+        roofline["note"] = "-e: no PMC instruction count measured for the endomorphism kernels; frac not computed"
     roofline["traffic"] = None
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         c_threads, hinfo = host_cores()
-        v = addr_cpu_baseline(text, args.cpu_seconds, c_threads, args.search)
+        v = addr_cpu_baseline(text, args.cpu_seconds, c_threads, search)
         cpu = {"value": round(v / 1e6, 4), "unit": "Mkeys/s", "cores": c_threads, "kind": "port",
                "sample": f"oracle ora_addr_group (thread_process group loop restatement, -l "
-                         f"{['uncompress', 'compress', 'both'][args.search]}), keys from 2^70, {args.cpu_seconds:.0f} s "
+                         f"{['uncompress', 'compress', 'both'][args.search]}{' -e' if args.endo else ''}), keys from 2^70, "
+                         f"{args.cpu_seconds:.0f} s "
                          f"on {c_threads} threads", "host": hinfo}
     out = {
         "metric": "Mkeys/s (-m address: keys hashed and bloom-probed per second) on 1/2/4/8 MI355X",
@@ -699,8 +709,11 @@ def bench_address(args, world, rank, dist, torch, lib_rec):
         "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": "real target file tests/unsolvedpuzzles.rmd (the reference's, committed as a fixture), -b 71 range "
                 "[2^70, 2^71) split into static rank blocks, sequential 2^32-key chunks",
-        "config": {"workload": "-m address -f tests/unsolvedpuzzles.rmd -l %s -b 71 (BASELINE configs[4])"
-                               % ["uncompress", "compress", "both"][args.search],
+        "config": {"workload": "-m address -f tests/unsolvedpuzzles.rmd -l %s%s -b 71 (BASELINE configs[4]%s)"
+                               % (["uncompress", "compress", "both"][args.search], " -e" if args.endo else "",
+                                  " with -e" if args.endo else ""),
+                   "endomorphism": args.endo,
+                   "reference_stat_keys_per_s": round(rate * (6 if args.endo else (2 if args.search == 1 else 1))),
                    "targets": len(A.table()), "n_seq": hex(n_seq), "chunks_per_step": chunks,
                    "keys_per_step": chunks * n_seq, "parallelism": "range-partition x%d" % world,
                    "table_build_s": round(t_build, 2), "bloom_hits": st["hits"], "found": len(found),

@@ -123,3 +123,31 @@ def test_bench_gpus_8_launch_check():
     assert d["n_gpus"] == 8
     assert [v["rank"] for v in d["ranks"]] == list(range(8))
     assert len({v["pid"] for v in d["ranks"]}) == 8
+
+
+def test_bench_refuses_unnamed_library_dir(tmp_path):
+    """KHB_LIB_DIR pointing away from the in-tree build is refused before any rank starts unless
+    --variant names the build (whose line is then marked); the in-tree directory itself is accepted."""
+    r = _bench(["--gpus", "1", "--launch-check"], _clean_env(KHB_LIB_DIR=str(tmp_path)))
+    assert r.returncode != 0 and r.stdout.strip() == ""
+    assert "--variant" in r.stderr and str(tmp_path) in r.stderr
+    r = _bench(["--gpus", "1", "--launch-check", "--variant", "x"], _clean_env(KHB_LIB_DIR=str(tmp_path)))
+    assert r.returncode == 0, r.stderr
+    r = _bench(["--gpus", "1", "--launch-check"], _clean_env(KHB_LIB_DIR=os.path.join(REPO, "keyhuntm1cpu_amd", "lib")))
+    assert r.returncode == 0, r.stderr
+
+
+def test_bench_records_the_loaded_library():
+    """bench.lib_record: the line's config names the loaded libkhbsgs.so (path, sha256 prefix, khb_build_info) and
+    refuses a build that says it is not the product when no --variant is given."""
+    import argparse
+    import hashlib
+    sys.path.insert(0, REPO)
+    import bench
+    rec = bench.lib_record(argparse.Namespace(variant=None))
+    with open(os.path.join(REPO, "keyhuntm1cpu_amd", "lib", "libkhbsgs.so"), "rb") as f:
+        assert rec["lib_sha16"] == hashlib.sha256(f.read()).hexdigest()[:16]
+    assert rec["lib_path"] == "keyhuntm1cpu_amd/lib/libkhbsgs.so"
+    assert rec["build"]["variant"] == "product" and rec["build"]["abi"] == "7"
+    with pytest.raises(SystemExit):
+        bench.lib_record(argparse.Namespace(variant="half"))     # the product build is not variant "half"

@@ -60,12 +60,14 @@ def test_trace_union_cli_uses_the_last_launches(tmp_path):
 def _pmc(d, dispatches):
     os.makedirs(d, exist_ok=True)
     with open(os.path.join(d, "pmc_counter_collection.csv"), "w", newline="") as f:
-        w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Grid_Size", "Kernel_Name", "Workgroup_Size", "Counter_Name",
+                                          "Counter_Value"])
         w.writeheader()
         for did, counters in dispatches:
             for k, v in counters.items():
-                w.writerow({"Dispatch_Id": did, "Kernel_Name": "void khbk::k_giant_scan<7>(khbk::ScanArgs)",
-                            "Counter_Name": k, "Counter_Value": v})
+                w.writerow({"Dispatch_Id": did, "Grid_Size": 262144, "Workgroup_Size": 256,
+                            "Kernel_Name": "void khbk::k_giant_scan<8>(khbk::ScanArgs)", "Counter_Name": k,
+                            "Counter_Value": v})
 
 
 def test_pmc_summary_corrections(tmp_path):
@@ -95,6 +97,24 @@ def test_pmc_summary_corrections(tmp_path):
     assert d["hbm_bytes_per_launch"] == 96 * steps
     assert d["valu_instr_per_giant_step"] == 700.0
     assert d["valu_busy_pct"] == 100.0
+    # the configuration comes from the dispatch (grid 262,144 lanes, k_giant_scan<8> = kScanG1) and the library
+    assert (d["lanes"], d["waves_per_simd"], d["level0_gate"], d["kernel_mode"]) == (262144, 4, True, 8)
+    assert d["kernel_build"]["variant"] == "product"
+    assert d["algorithmic_bytes_per_giant_step"] == (24 if d["kernel_build"]["half_stream"] == "1" else 40)
+
+
+def test_pmc_summary_refuses_a_dispatch_without_its_configuration(tmp_path):
+    """a PMC CSV whose k_giant_scan rows lack the grid size is an error, not a default."""
+    d = tmp_path / "pmc_fetch_0"
+    os.makedirs(d)
+    with open(d / "pmc_counter_collection.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        w.writerow({"Dispatch_Id": 1, "Kernel_Name": "void khbk::k_giant_scan<8>(khbk::ScanArgs)",
+                    "Counter_Name": "FETCH_SIZE", "Counter_Value": 1.0})
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"), str(tmp_path), "1",
+                        str(tmp_path / "o.json")], capture_output=True, text=True)
+    assert r.returncode != 0 and "grid size" in (r.stderr + r.stdout)
 
 
 def test_committed_pmc_latest_reproduces_from_its_csvs(tmp_path):
@@ -193,8 +213,11 @@ def test_pmc_record_attaches_only_to_its_configuration():
     with open(os.path.join(REPO, "profiles", "pmc_latest.json")) as f:
         pmc = json.load(f)
     default = {"k": 1, "level0_gate": True, "lanes": 262144, "waves_per_simd": 4}
+    if "kernel_build" in pmc:
+        default["kernel_build"] = pmc["kernel_build"]
     assert bench.pmc_mismatch(pmc, default) is None
-    for change in ({"level0_gate": False}, {"k": 4}, {"lanes": 196608, "waves_per_simd": 3}):
+    for change in ({"level0_gate": False}, {"k": 4}, {"lanes": 196608, "waves_per_simd": 3},
+                   {"kernel_build": {"variant": "half", "half_stream": "0"}}):
         note = bench.pmc_mismatch(pmc, dict(default, **change))
         assert note and "not measured for this run" in note and all(k in note for k in change)
     assert bench.pmc_mismatch({"k": 1}, default)          # a record without its configuration never matches
