@@ -149,11 +149,8 @@ def power_sampler(torch, local: int, args):
     from keyhuntm1cpu_amd.power import PowerSampler
     if args.no_power:
         return PowerSampler.disabled("--no-power")
-    try:
-        bus = torch.cuda.get_device_properties(local).pci_bus_id
-    except Exception:                                  # noqa: BLE001
-        bus = None
-    return PowerSampler(bus)
+    bdf = physical_gpu(torch, local)                   # "dddd:bb:dd" (full domain:bus:device)
+    return PowerSampler(None if bdf.startswith("device") else bdf)
 
 
 def physical_gpu(torch, local: int) -> str:

@@ -27,26 +27,40 @@ def _num(v):
         return None
 
 
-def _handle_for_bus(amdsmi, pci_bus: int | None):
+def _bdf_key(bdf: str) -> tuple[int, int, int] | None:
+    """(domain, bus, device) of "dddd:bb:dd[.f]" (amdsmi's BDF and bench.physical_gpu's PCI address)."""
+    try:
+        dom, bus, rest = bdf.strip().split(":")
+        return int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16)
+    except (AttributeError, ValueError):
+        return None
+
+
+def _handle_for_bdf(amdsmi, bdf: str | None):
+    """The amdsmi handle of the GPU at PCI address `bdf` ("dddd:bb:dd", the full domain:bus:device).  No
+    match is an error (the power block is then unavailable), never another GPU's handle; with no address given only a
+    one-GPU system has an unambiguous handle."""
     hs = amdsmi.amdsmi_get_processor_handles()
     if not hs:
         return None, "no amdsmi GPU handles"
-    if pci_bus is None or len(hs) == 1:
-        return hs[0], None
+    want = _bdf_key(bdf) if bdf else None
+    if want is None:
+        if len(hs) == 1:
+            return hs[0], None
+        return None, "no PCI address for this rank's GPU and %d amdsmi handles" % len(hs)
     for h in hs:
         try:
-            bdf = amdsmi.amdsmi_get_gpu_device_bdf(h)        # "dddd:bb:dd.f"
-            if int(bdf.split(":")[1], 16) == pci_bus:
+            if _bdf_key(amdsmi.amdsmi_get_gpu_device_bdf(h)) == want:
                 return h, None
         except Exception:                                  # noqa: BLE001 - a handle we cannot read is skipped
             continue
-    return hs[0], "no handle on PCI bus %#x; using the first" % pci_bus
+    return None, "no amdsmi handle at PCI %s" % bdf
 
 
 class PowerSampler:
-    """with PowerSampler(pci_bus) as ps: <timed region>;  ps.summary() -> dict."""
+    """with PowerSampler(bdf) as ps: <timed region>;  ps.summary() -> dict.  bdf: the GPU's "dddd:bb:dd"."""
 
-    def __init__(self, pci_bus: int | None = None, period: float = 0.05):
+    def __init__(self, bdf: str | None = None, period: float = 0.05):
         self.period = period
         self.samples = []
         self.err = None
@@ -58,7 +72,7 @@ class PowerSampler:
             import amdsmi
             amdsmi.amdsmi_init()
             self.amdsmi = amdsmi
-            self.h, note = _handle_for_bus(amdsmi, pci_bus)
+            self.h, note = _handle_for_bdf(amdsmi, bdf)
             if self.h is None:
                 self.err = note
             else:

@@ -221,3 +221,28 @@ def test_pmc_record_attaches_only_to_its_configuration():
         note = bench.pmc_mismatch(pmc, dict(default, **change))
         assert note and "not measured for this run" in note and all(k in note for k in change)
     assert bench.pmc_mismatch({"k": 1}, default)          # a record without its configuration never matches
+
+
+def test_power_handle_matches_full_pci_address():
+    """the amdsmi handle is matched on the full domain:bus:device, and a rank whose GPU is not found gets
+    no power block instead of another GPU's figures."""
+    sys.path.insert(0, REPO)
+    from keyhuntm1cpu_amd.power import _handle_for_bdf
+
+    class FakeSmi:
+        bdfs = {"h0": "0000:8b:00.0", "h1": "0001:8b:00.0", "h2": "0000:8b:01.0"}
+
+        def amdsmi_get_processor_handles(self):
+            return list(self.bdfs)
+
+        def amdsmi_get_gpu_device_bdf(self, h):
+            return self.bdfs[h]
+    smi = FakeSmi()
+    assert _handle_for_bdf(smi, "0001:8b:00") == ("h1", None)       # same bus, other domain
+    assert _handle_for_bdf(smi, "0000:8b:01") == ("h2", None)       # same bus, other device
+    h, why = _handle_for_bdf(smi, "0000:9c:00")
+    assert h is None and "0000:9c:00" in why
+    h, why = _handle_for_bdf(smi, None)
+    assert h is None and "3 amdsmi handles" in why
+    FakeSmi.bdfs = {"h0": "0000:8b:00.0"}
+    assert _handle_for_bdf(FakeSmi(), None) == ("h0", None)
