@@ -91,7 +91,12 @@ constexpr bool is_dump(int m) { return m == kDump || m == kAddrDump || m == kBab
 #ifndef KHB_ADDR_WAVES_PER_SIMD
 #define KHB_ADDR_WAVES_PER_SIMD KHB_WAVES_PER_SIMD   // occupancy target of the -m address hash kernels
 #endif
-constexpr int waves_per_simd(int m) { return is_addr(m) ? KHB_ADDR_WAVES_PER_SIMD : KHB_WAVES_PER_SIMD; }
+#ifndef KHB_ADDR_E_WAVES_PER_SIMD
+#define KHB_ADDR_E_WAVES_PER_SIMD KHB_ADDR_WAVES_PER_SIMD   // occupancy target of the -e address kernels
+#endif
+constexpr int waves_per_simd(int m) {
+  return is_endo(m) ? KHB_ADDR_E_WAVES_PER_SIMD : is_addr(m) ? KHB_ADDR_WAVES_PER_SIMD : KHB_WAVES_PER_SIMD;
+}
 constexpr uint32_t kHalf = KHB_GROUP / 2;            // 512
 constexpr uint32_t kCandCap = 1u << 20;
 constexpr uint32_t kAddrHitCap = 1u << 18;

@@ -7,7 +7,11 @@
 // Modes: add_u32 mov_b32 alignbit addc_vcc mad64 mad_addc (the field product's pair: v_mad_u64_u32 -> VCC, s_nop 0,
 //        v_addc_co_u32) nop fma_f64 sleep | stream (non-temporal 32-B per lane in, 32-B per lane out, [entry][lane]
 //        like the prefix scratch) | gather_l2 / gather_mall / gather_hbm (one 8-B load per lane per step from a 2 MiB /
-//        32 MiB / 4 GiB table at a hashed index, as the level-0 gate)
+//        32 MiB / 4 GiB table at a hashed index, as the level-0 gate) | salu (s_add_u32 chains, per wave-instruction) |
+//        smem (s_load_dwordx8 of 32-B rows of a 64 KiB table, wave-uniform: the GSn rows, per wave-load) | lds (one
+//        ds_write_b32 + one ds_read_b32 per lane per step, per lane-access) | scratch (one scratch store + one scratch
+//        load of 4 B per lane per step into a private array indexed by the step: the spill pattern, per lane-access)
+//        (round 6: the classes of VERDICT r5 item 5's energy split)
 // Usage: ./valu_energy <mode> <seconds>
 #include <hip/hip_runtime.h>
 #include <chrono>
@@ -57,6 +61,73 @@ __global__ __launch_bounds__(256, 4) void k_alu(uint64_t* out, uint32_t s) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) r ^= x[i] ^ y[i] ^ (uint64_t)f[i];
   if (r == 0x12345) out[0] = r;
+}
+
+// SALU: 16 independent s_add_u32 chains per wave (one wave-instruction each per body)
+__global__ __launch_bounds__(256, 4) void k_salu(uint64_t* out, uint32_t s) {
+  uint32_t a0 = s, a1 = s + 1, a2 = s + 2, a3 = s + 3, a4 = s + 4, a5 = s + 5, a6 = s + 6, a7 = s + 7;
+  uint32_t b0 = s * 3, b1 = s * 5, b2 = s * 7, b3 = s * 9, b4 = s * 11, b5 = s * 13, b6 = s * 15, b7 = s * 17;
+  for (int it = 0; it < ITERS; ++it) {
+    asm volatile("s_add_u32 %0, %0, %16\n\ts_add_u32 %1, %1, %16\n\ts_add_u32 %2, %2, %16\n\ts_add_u32 %3, %3, %16\n\t"
+                 "s_add_u32 %4, %4, %16\n\ts_add_u32 %5, %5, %16\n\ts_add_u32 %6, %6, %16\n\ts_add_u32 %7, %7, %16\n\t"
+                 "s_add_u32 %8, %8, %16\n\ts_add_u32 %9, %9, %16\n\ts_add_u32 %10, %10, %16\n\ts_add_u32 %11, %11, %16\n\t"
+                 "s_add_u32 %12, %12, %16\n\ts_add_u32 %13, %13, %16\n\ts_add_u32 %14, %14, %16\n\ts_add_u32 %15, %15, %16"
+                 : "+s"(a0), "+s"(a1), "+s"(a2), "+s"(a3), "+s"(a4), "+s"(a5), "+s"(a6), "+s"(a7), "+s"(b0), "+s"(b1),
+                   "+s"(b2), "+s"(b3), "+s"(b4), "+s"(b5), "+s"(b6), "+s"(b7)
+                 : "s"(s)
+                 : "scc");
+  }
+  const uint32_t r = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7 ^ b0 ^ b1 ^ b2 ^ b3 ^ b4 ^ b5 ^ b6 ^ b7;
+  if (r == 0x12345u && threadIdx.x == 0) out[0] = r;
+}
+
+// SMEM: wave-uniform 32-B rows of a 64 KiB table through the constant address space (s_load_dwordx8), as the walk
+// reads GSn[i]; the row index walks the table, 8 loads in flight per body
+__global__ __launch_bounds__(256, 4) void k_smem(const __attribute__((address_space(4))) uint32_t* tab, uint64_t* out,
+                                                 uint32_t s) {
+  uint32_t acc = 0;
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t row = (uint32_t)(it * 8 + k + s) & 2047u;      // 2048 rows x 32 B = 64 KiB
+      const __attribute__((address_space(4))) uint32_t* p = tab + 8 * row;
+      acc += p[0] ^ p[1] ^ p[2] ^ p[3] ^ p[4] ^ p[5] ^ p[6] ^ p[7];
+    }
+  }
+  if (acc == 0x12345u) out[0] = acc + threadIdx.x;
+}
+
+// LDS: per lane one 4-B write and one 4-B read per step, 16 steps per body (the survivor queue's accesses)
+__global__ __launch_bounds__(256, 4) void k_lds(uint64_t* out, uint32_t s) {
+  __shared__ uint32_t buf[256 * 16];
+  uint32_t acc = threadIdx.x ^ s;
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      volatile __attribute__((address_space(3))) uint32_t* q =
+          (volatile __attribute__((address_space(3))) uint32_t*)(buf + k * 256 + threadIdx.x);
+      *q = acc + k;
+      acc ^= *q;
+    }
+  }
+  if (acc == 0x12345u) out[0] = acc;
+}
+
+// scratch: per lane one 4-B store and one 4-B load of a private array indexed by a runtime value (the compiler
+// keeps it in scratch memory: the spill pattern, which the product's waves reach through the L1/L2)
+__global__ __launch_bounds__(256, 4) void k_scratch(uint64_t* out, uint32_t s) {
+  uint32_t arr[64];
+  volatile __attribute__((address_space(5))) uint32_t* priv = (volatile __attribute__((address_space(5))) uint32_t*)arr;
+  uint32_t acc = threadIdx.x ^ s;
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t i = (acc + (uint32_t)k) & 63u;
+      priv[i] = acc;
+      acc += priv[(i + 7u) & 63u];
+    }
+  }
+  if (acc == 0x12345u) out[0] = acc;
 }
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -109,7 +180,10 @@ int main(int argc, char** argv) {
     steps = 4096;
     CHECK(hipMalloc(&buf, bytes));
     CHECK(hipMemset(buf, 0x5a, bytes));
-  } else if (alu < 0) {
+  } else if (mode == "smem") {
+    CHECK(hipMalloc(&buf, 64 * 1024));
+    CHECK(hipMemset(buf, 0x3c, 64 * 1024));
+  } else if (alu < 0 && mode != "salu" && mode != "lds" && mode != "scratch") {
     printf("unknown mode %s\n", mode.c_str());
     return 2;
   }
@@ -121,6 +195,12 @@ int main(int argc, char** argv) {
       default: break;
     }
     if (mode == "stream") hipLaunchKernelGGL(k_stream, dim3(blocks), dim3(256), 0, 0, (v4u*)buf, entries, lanes, out);
+    else if (mode == "salu") hipLaunchKernelGGL(k_salu, dim3(blocks), dim3(256), 0, 0, out, s);
+    else if (mode == "smem")
+      hipLaunchKernelGGL(k_smem, dim3(blocks), dim3(256), 0, 0,
+                         (const __attribute__((address_space(4))) uint32_t*)buf, out, s);
+    else if (mode == "lds") hipLaunchKernelGGL(k_lds, dim3(blocks), dim3(256), 0, 0, out, s);
+    else if (mode == "scratch") hipLaunchKernelGGL(k_scratch, dim3(blocks), dim3(256), 0, 0, out, s);
     else hipLaunchKernelGGL(k_gather, dim3(blocks), dim3(256), 0, 0, (const uint2*)buf, mask, steps, out);
   };
   launch(1);
@@ -138,6 +218,9 @@ int main(int argc, char** argv) {
   const char* unit = "lane_instr";
   if (alu >= 0) units = (double)lanes * ITERS * 16 * kPer[alu];
   else if (mode == "stream") { units = (double)lanes * entries * 64; unit = "byte"; }
+  else if (mode == "salu") { units = (double)(lanes / 64) * ITERS * 16; unit = "wave_instr"; }
+  else if (mode == "smem") { units = (double)(lanes / 64) * ITERS * 8; unit = "wave_load_32B"; }
+  else if (mode == "lds" || mode == "scratch") { units = (double)lanes * ITERS * 16 * 2; unit = "lane_access_4B"; }
   else { units = (double)lanes * steps; unit = "load"; }
   if (alu == NOP || alu == SLEEP) units = (double)lanes * ITERS * 16, unit = "lane_slot";
   printf("{\"mode\": \"%s\", \"launches\": %llu, \"seconds\": %.3f, \"unit\": \"%s\", \"units_per_s\": %.6e}\n",
