@@ -10,7 +10,9 @@
 //        32 MiB / 4 GiB table at a hashed index, as the level-0 gate) | salu (s_add_u32 chains, per wave-instruction) |
 //        smem (s_load_dwordx8 of 32-B rows of a 64 KiB table, wave-uniform: the GSn rows, per wave-load) | lds (one
 //        ds_write_b32 + one ds_read_b32 per lane per step, per lane-access) | scratch (one scratch store + one scratch
-//        load of 4 B per lane per step into a private array indexed by the step: the spill pattern, per lane-access)
+//        load of 4 B per lane per step into a 256-B private array at a data-dependent index: 64 MiB over the chip, so
+//        mostly MALL, per lane-access) | scratch_l2 (8-B reload + store of 8 fixed slots per lane: the product's
+//        spill pattern, L2-resident, per lane-access)
 //        (round 6: the classes of VERDICT r5 item 5's energy split)
 // Usage: ./valu_energy <mode> <seconds>
 #include <hip/hip_runtime.h>
@@ -130,6 +132,24 @@ __global__ __launch_bounds__(256, 4) void k_scratch(uint64_t* out, uint32_t s) {
   if (acc == 0x12345u) out[0] = acc;
 }
 
+// scratch_l2: the product's spill pattern -- a few fixed 8-B slots per lane (8 here, 64 B per lane: 16 MiB over the
+// chip, 2 MiB per XCD, L2-resident), stored and reloaded at fixed offsets
+__global__ __launch_bounds__(256, 4) void k_scratch_l2(uint64_t* out, uint32_t s) {
+  uint64_t arr[8];
+  volatile __attribute__((address_space(5))) uint64_t* priv = (volatile __attribute__((address_space(5))) uint64_t*)arr;
+  uint64_t acc = threadIdx.x ^ s;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) priv[k] = acc + k;
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      acc += priv[k & 7];
+      priv[(k + 3) & 7] = acc;
+    }
+  }
+  if (acc == 0x12345u) out[0] = acc;
+}
+
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 // the prefix scratch's pattern: [entry][lane] 32-B entries, non-temporal; per step each lane stores one entry and
 // loads one written `lag` entries earlier (streaming, no reuse)
@@ -183,7 +203,7 @@ int main(int argc, char** argv) {
   } else if (mode == "smem") {
     CHECK(hipMalloc(&buf, 64 * 1024));
     CHECK(hipMemset(buf, 0x3c, 64 * 1024));
-  } else if (alu < 0 && mode != "salu" && mode != "lds" && mode != "scratch") {
+  } else if (alu < 0 && mode != "salu" && mode != "lds" && mode != "scratch" && mode != "scratch_l2") {
     printf("unknown mode %s\n", mode.c_str());
     return 2;
   }
@@ -201,6 +221,7 @@ int main(int argc, char** argv) {
                          (const __attribute__((address_space(4))) uint32_t*)buf, out, s);
     else if (mode == "lds") hipLaunchKernelGGL(k_lds, dim3(blocks), dim3(256), 0, 0, out, s);
     else if (mode == "scratch") hipLaunchKernelGGL(k_scratch, dim3(blocks), dim3(256), 0, 0, out, s);
+    else if (mode == "scratch_l2") hipLaunchKernelGGL(k_scratch_l2, dim3(blocks), dim3(256), 0, 0, out, s);
     else hipLaunchKernelGGL(k_gather, dim3(blocks), dim3(256), 0, 0, (const uint2*)buf, mask, steps, out);
   };
   launch(1);
@@ -221,6 +242,7 @@ int main(int argc, char** argv) {
   else if (mode == "salu") { units = (double)(lanes / 64) * ITERS * 16; unit = "wave_instr"; }
   else if (mode == "smem") { units = (double)(lanes / 64) * ITERS * 8; unit = "wave_load_32B"; }
   else if (mode == "lds" || mode == "scratch") { units = (double)lanes * ITERS * 16 * 2; unit = "lane_access_4B"; }
+  else if (mode == "scratch_l2") { units = (double)lanes * ITERS * 16 * 2; unit = "lane_access_8B"; }
   else { units = (double)lanes * steps; unit = "load"; }
   if (alu == NOP || alu == SLEEP) units = (double)lanes * ITERS * 16, unit = "lane_slot";
   printf("{\"mode\": \"%s\", \"launches\": %llu, \"seconds\": %.3f, \"unit\": \"%s\", \"units_per_s\": %.6e}\n",

@@ -14,7 +14,7 @@ from keyhuntm1cpu_amd.power import PowerSampler  # noqa: E402
 
 BIN = os.path.join(REPO, "tools", "microbench", "valu_energy")
 MODES = ["sleep", "nop", "add_u32", "mov_b32", "alignbit", "addc_vcc", "mad64", "mad_addc", "fma_f64", "stream",
-         "gather_l2", "gather_mall", "gather_hbm", "salu", "smem", "lds", "scratch", "sleep"]
+         "gather_l2", "gather_mall", "gather_hbm", "salu", "smem", "lds", "scratch", "scratch_l2", "sleep"]
 
 
 def main():
