@@ -47,8 +47,17 @@ OPS_PER_STEP = (2561 * MUL_OPS + 1023 * SQR_OPS + INV_OPS) / 1024.0 + 2 * 66 + 2
 # The multiply-class work this kernel executes per giant step: per group 511 forward
 # prefix products + the walk's 2045 products and 1023 squarings (walk_group_g) + 9 products and one
 # squaring of the work item's centre and chained-product bookkeeping (scan_batch), and two inversions
-# per 8-group work item; no XXH64 / "% bits" for the 99.96 % of x the level-0 gate stops.
-EXEC_OPS_PER_STEP = ((2556 + 9) * MUL_OPS + (1023 + 1) * SQR_OPS) / 1024.0 + 2 * INV_OPS / (8 * 1024.0)
+# per 8-group work item; no XXH64 / "% bits" for the 99.96 % of x the level-0 gate stops.  The half prefix
+# stream (KHB_HALF_STREAM, the product since round 6) rebuilds every even prefix in the walk: 255 more
+# products per group (walk_group_g_half: one per pair of walk steps but the last, plus the peeled step 511).
+HALF_STREAM_MULS = 255
+EXEC_OPS_PER_STEP_FULL = ((2556 + 9) * MUL_OPS + (1023 + 1) * SQR_OPS) / 1024.0 + 2 * INV_OPS / (8 * 1024.0)
+EXEC_OPS_PER_STEP = EXEC_OPS_PER_STEP_FULL + HALF_STREAM_MULS * MUL_OPS / 1024.0
+
+
+def exec_ops_per_step(build: dict) -> float:
+    """Executed multiply-class ops per giant step of the loaded build (khb_build_info's half_stream)."""
+    return EXEC_OPS_PER_STEP if build.get("half_stream", "1") == "1" else EXEC_OPS_PER_STEP_FULL
 # Peak of the binding unit: v_mad_u64_u32 issue rate measured on MI355X by tools/microbench/intops2.hip
 # at full occupancy, 57.8 lane-ops/clk/CU at the 2.16 GHz the microbenchmark ran at
 # (profiles/r01_intops2.txt); the same rate at the 2.4 GHz peak engine clock is 35.5 T.
@@ -446,7 +455,8 @@ def main():
         time_basis = "ms_per_step (the launches' event intervals were unavailable)"
     achieved = OPS_PER_STEP * per_launch_steps / (bmax * 1e-3) / 1e12
     achieved_launch = OPS_PER_STEP * per_launch_steps / (max(kmax, 1e-9) * 1e-3) / 1e12
-    executed = EXEC_OPS_PER_STEP * per_launch_steps / (bmax * 1e-3) / 1e12
+    exec_ops = exec_ops_per_step(lib_rec["build"])
+    executed = exec_ops * per_launch_steps / (bmax * 1e-3) / 1e12
     mhz = st["shader_mhz"]
     peak_at_clock = PEAK_LANES_PER_CLK_CU * CUS * mhz * 1e6 / 1e12 if mhz > 0 else None
     roofline = {"bound": "valu", "unit": "Tops/s", "achieved": round(achieved, 3), "peak": PEAK_MULOPS_T,
@@ -471,10 +481,10 @@ def main():
                 "frac_at_2p16ghz": round(achieved / PEAK_MULOPS_T_2P16, 4),
                 "peak_at_shader_clock": round(peak_at_clock, 3) if peak_at_clock else None,
                 "frac_at_shader_clock": round(achieved / peak_at_clock, 4) if peak_at_clock else None}
-    executed_info = {"ops_per_giant_step": round(EXEC_OPS_PER_STEP, 2),
+    executed_info = {"ops_per_giant_step": round(exec_ops, 2),
                      "note": "multiply-class work the kernel performs: the reference's field work without the "
                              "3 of 4 inversions the 8-group batch saves and without the two XXH64 the level-0 "
-                             "gate skips for 99.96 % of x",
+                             "gate skips for 99.96 % of x, plus the half prefix stream's 255 products per group",
                      "achieved": round(executed, 3), "frac": round(executed / PEAK_MULOPS_T, 4),
                      "frac_at_2p16ghz": round(executed / PEAK_MULOPS_T_2P16, 4)}
     pmc_path = os.path.join(REPO, "profiles", "pmc_latest.json")
