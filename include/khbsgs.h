@@ -152,7 +152,7 @@ int khb_load_gate(khb_ctx* ctx, const uint8_t* gate, uint32_t log2_bits, uint32_
  * full gate only when those bits are all set: the same candidates, and most tests served by a fold
  * small enough for the L2 (k = 1) or by one that fits the Infinity Cache beside the level-1 bloom
  * (k >= 4).  0 = no stage 1; otherwise log2_bytes in [10, 31], or KHB_GATE_STAGE1_AUTO (the default):
- * 2 MiB for a gate of up to 32 MiB (k = 1), 16 MiB for a larger one (k >= 4). */
+ * 2 MiB for a gate of up to 32 MiB (k = 1), 32 MiB for a larger one (k >= 4). */
 #define KHB_GATE_STAGE1_AUTO 1
 int khb_set_gate_stage1(khb_ctx* ctx, uint32_t log2_bytes);
 /* Stage-0 filter for gates loaded after this call, in front of a stage-1 fold: the hi words of the gate's blocks

@@ -605,10 +605,11 @@ int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t 
   c->gate_mask = (uint32_t)((1ull << (log2_bits - 6)) - 1);
   c->gate_probes = probes;
   // KHB_GATE_STAGE1_AUTO: an L2-sized 2 MiB fold of a gate of up to 32 MiB (k = 1: -8.6 % time with two
-  // launches in flight, profiles/r04k/stage1_k1_nt_pipe_ab.txt), a 16 MiB fold of a larger one (k = 4: the
-  // 128 MiB gate beside the 57.5 MiB L1 bloom; 16 and 8 MiB -3.5 % vs 32 MiB with the non-temporal prefix
-  // stream, 4 MiB slower, profiles/r04l/k4_stage1_ab.txt)
-  const uint32_t f_log2 = c->gate1_log2 != KHB_GATE_STAGE1_AUTO ? c->gate1_log2 : bytes <= (1u << 25) ? 21u : 24u;
+  // launches in flight, profiles/r04k/stage1_k1_nt_pipe_ab.txt; 4 MiB equal on the half-stream product, r06d), a
+  // 32 MiB fold of a larger one (k = 4: the 128 MiB gate beside the 57.5 MiB L1 bloom).  Round 4 (full prefix stream)
+  // had measured 16 MiB 3.5 % faster than 32 MiB (profiles/r04l/k4_stage1_ab.txt); with the half prefix stream's
+  // halved MALL traffic 32 MiB is 1.3 % faster than 16 MiB and 0.8 % than 64 MiB (5 rounds each, profiles/r06e).
+  const uint32_t f_log2 = c->gate1_log2 != KHB_GATE_STAGE1_AUTO ? c->gate1_log2 : bytes <= (1u << 25) ? 21u : 25u;
   if (f_log2 && (size_t)1 << f_log2 < bytes) {
     // stage 1: the gate OR-folded to 2^f_log2 bytes (a superset: no member is ever dropped)
     const size_t nb1 = ((size_t)1 << f_log2) / 8, nb = bytes / 8;

@@ -221,8 +221,8 @@ def test_k4_full_geometry_candidates_match_oracle(tables_k4, ora):
     """Config C (-k 4, default -n): 2^24 baby steps, 57.5 MiB level-1 bloom.  Every candidate of two
     whole chunks (2 x 1024 groups) equals the oracle's, and the key comes back through the second
     check at k = 4 (M3 = 16384).  The level-0 gate's candidates are exactly the L1 candidates whose
-    gate bits are set (x from the GPU dump of their group), with no fold, a 32 MiB fold, the auto 16 MiB fold
-    (khb_set_gate_stage1), and the stage-0 filter in front of the 16 MiB or a 32 MiB fold (khb_set_gate_stage0,
+    gate bits are set (x from the GPU dump of their group), with no fold, a 16 MiB fold, the auto 32 MiB fold
+    (khb_set_gate_stage1), and the stage-0 filter in front of the 32 MiB or a 16 MiB fold (khb_set_gate_stage0,
     VERDICT r5 item 3; off in the product), and still hold the key."""
     from keyhuntm1cpu_amd.khbsgs import Engine
     bs = ora.Bsgs(None, 4)
@@ -241,9 +241,9 @@ def test_k4_full_geometry_candidates_match_oracle(tables_k4, ora):
         # the product gate at k = 4 (2^30 bits, 128 MiB) with and without its 32 MiB stage-1 fold
         gate, lg = tables_k4.gate()
         gated = {}
-        # (stage1, stage0): 1 = KHB_GATE_STAGE1_AUTO (16 MiB at k = 4: the product) / KHB_GATE_STAGE0_AUTO (the 2 MiB
+        # (stage1, stage0): 1 = KHB_GATE_STAGE1_AUTO (32 MiB at k = 4: the product) / KHB_GATE_STAGE0_AUTO (the 2 MiB
         # filter in front of it, kScanG2: exact, but measured slower and off by default)
-        stages = ((0, 0), (25, 0), (1, 0), (1, 1), (25, 22))
+        stages = ((0, 0), (24, 0), (1, 0), (1, 1), (24, 22))
         for stage1, stage0 in stages:
             e.set_gate_stage1(stage1)
             e.set_gate_stage0(stage0)
