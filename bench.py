@@ -589,6 +589,10 @@ def main():
 # half-rate (v_alignbit_b32, v_add3_u32, v_mad_u64_u32: ~4.6), profiles/r03_valu_cost.txt and
 # tools/debug/bb_path.py over tools/microbench/hash_isa.hip = 3.73 cycles per wave-instruction.
 ADDR_EXEC_VALU_PER_KEY = {2: 9256.1}
+# With -e (-l both): SQ_INSTS_VALU x 64 / keys of a two-chunk launch of k_giant_scan<kAddrBE> (tools/addr_floor.py with
+# SEARCH=6 under rocprofv3, profiles/r06h/addr_s6: 4.9495e12 x 64 / 2^33 = 36,877.0 per key; the plain kernel's
+# count in the same call, 9,259.8, reproduces the value above).  Twelve hashes per key instead of three.
+ADDR_EXEC_VALU_PER_KEY_ENDO = {2: 36877.0}
 # The VALU floor per key of -l both, in the same unit: the hash blocks as compiled alone
 # (tools/microbench/hash_isa.hip -> profiles/r02_hash_isa_counts.txt: the 02/03 compressed hash160 pair
 # 4,401, the uncompressed hash160 3,616, XXH64 of three 20-byte hashes 3 x 137 / 2) plus the x/y walk,
@@ -678,7 +682,7 @@ def bench_address(args, world, rank, dist, torch, lib_rec):
     roofline = {"bound": "valu", "unit": "T lane-instr/s", "kernel": "k_giant_scan<address>",
                 "time_basis": "wall time of the timed steps (two launches in flight, as the CLI runs them)",
                 "shader_mhz_avg": round(mhz, 1)}
-    e = None if args.endo else ADDR_EXEC_VALU_PER_KEY.get(args.search)
+    e = (ADDR_EXEC_VALU_PER_KEY_ENDO if args.endo else ADDR_EXEC_VALU_PER_KEY).get(args.search)
     if e and mhz > 0:
         peak = CUS * 4 * 64 / ADDR_MIX_CYCLES_PER_INSTR * mhz * 1e6 / 1e12
         ach = e * per_gpu / 1e12
@@ -687,7 +691,8 @@ def bench_address(args, world, rank, dist, torch, lib_rec):
                          "peak_basis": "the hash mix's issue ceiling, %.2f SIMD cycles per wave-instruction (43 %% "
                                        "full-rate / 57 %% half-rate VALU, profiles/r03_valu_cost.txt) x 1024 SIMDs at "
                                        "the launches' measured shader clock" % ADDR_MIX_CYCLES_PER_INSTR,
-                         "executed_source": "profiles/r04b/addr_libkhbsgs (PMC SQ_INSTS_VALU, tools/addr_floor.py)"})
+                         "executed_source": ("profiles/r06h/addr_s6" if args.endo else "profiles/r04b/addr_libkhbsgs")
+                                            + " (PMC SQ_INSTS_VALU, tools/addr_floor.py)"})
         fl = None if args.endo else ADDR_FLOOR_TERMS.get(args.search)
         if fl:
             floor = sum(fl.values())
@@ -697,8 +702,8 @@ def bench_address(args, world, rank, dist, torch, lib_rec):
                                             "walk's PMC count in the hash-less build (profiles/r04b)"})
     if not args.endo:
         roofline["algorithmic_ops_per_key"] = ADDR_ALG_OPS[args.search]
-    else:
-        roofline["note"] = "-e: no PMC instruction count measured for the endomorphism kernels; frac not computed"
+    elif e is None:
+        roofline["note"] = "-e: no PMC instruction count measured for this -l mode's endomorphism kernel; frac not computed"
     roofline["traffic"] = None
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
