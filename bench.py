@@ -284,7 +284,9 @@ def main():
     # WORLD_SIZE must equal N; run bare with N > 1, the ranks are started here as child processes before
     # anything touches the GPU (keyhuntm1cpu_amd/launch.py), and this process only forwards rank 0's line.
     from keyhuntm1cpu_amd import launch
-    launch.main_or_spawn(args.gpus, sys.argv[1:], os.path.abspath(__file__))
+    # rank 0 runs the CPU baseline alone after the other ranks return (only at N = 1, but the budget is passed anyway)
+    cpu_budget = 0.0 if args.no_cpu_baseline else args.cpu_seconds * max(1, args.cpu_windows) + 120.0
+    launch.main_or_spawn(args.gpus, sys.argv[1:], os.path.abspath(__file__), rank0_extra_s=cpu_budget)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -76,14 +76,16 @@ def _kill_group(p: subprocess.Popen, sig: int):
 
 
 def spawn_ranks(world: int, cmd: Sequence[str], env: Mapping[str, str] | None = None, grace_s: float = 15.0,
-                straggler_s: float = 300.0, timeout_s: float | None = None) -> int:
+                straggler_s: float = 300.0, timeout_s: float | None = None, rank0_grace_s: float | None = None) -> int:
     """Run `cmd` as `world` rank processes; rank 0's stdout is forwarded to ours, the other ranks' stdout
     goes to our stderr (stdout keeps exactly rank 0's JSON line).  When a rank fails, the others are
     terminated (SIGTERM, then SIGKILL after grace_s) and its exit status is returned; 0 when all succeed.
     Once rank 0 has exited cleanly, the others have straggler_s to follow (rank 0 is the last to need them:
     bench.py's other ranks return after the final all_gather and rank 0 alone goes on to the CPU baseline, so
     only a rank still running after rank 0 is stuck); with timeout_s the whole run has that long.
-    Either limit stops the remaining ranks the same way and returns 124, as timeout(1) does."""
+    Rank 0 itself, once every other rank has exited cleanly, has rank0_grace_s (bench.py: its CPU-baseline budget
+    plus straggler_s) before it is taken to be stuck.  Either limit stops the remaining ranks the same way and
+    returns 124, as timeout(1) does."""
     base = dict(os.environ if env is None else env)
     port = free_port()
     procs: list[subprocess.Popen] = []
@@ -106,6 +108,7 @@ def spawn_ranks(world: int, cmd: Sequence[str], env: Mapping[str, str] | None = 
         live = set(range(world))
         t_start = time.time()
         first_exit = None                          # when rank 0 exited cleanly
+        others_done = None                         # when every rank but 0 had exited cleanly
 
         def stop_live():
             for q in live:
@@ -136,11 +139,14 @@ def spawn_ranks(world: int, cmd: Sequence[str], env: Mapping[str, str] | None = 
             if not live:
                 break
             now = time.time()
+            if others_done is None and live == {0} and rc == 0:
+                others_done = now
             late = first_exit is not None and now - first_exit > straggler_s
-            if late or (timeout_s is not None and now - t_start > timeout_s):
-                print(f"[bench] ranks {sorted(live)} still running "
-                      + (f"{straggler_s:.0f} s after another rank exited" if late else f"after {timeout_s:.0f} s")
-                      + "; stopping them", file=sys.stderr, flush=True)
+            late0 = rank0_grace_s is not None and others_done is not None and now - others_done > rank0_grace_s
+            if late or late0 or (timeout_s is not None and now - t_start > timeout_s):
+                why = (f"{straggler_s:.0f} s after rank 0 exited" if late else
+                       f"{rank0_grace_s:.0f} s after the other ranks exited" if late0 else f"after {timeout_s:.0f} s")
+                print(f"[bench] ranks {sorted(live)} still running {why}; stopping them", file=sys.stderr, flush=True)
                 stop_live()
                 rc = rc or 124
                 break
@@ -157,12 +163,14 @@ def spawn_ranks(world: int, cmd: Sequence[str], env: Mapping[str, str] | None = 
     return rc
 
 
-def main_or_spawn(gpus: int, argv: Sequence[str], script: str) -> str:
+def main_or_spawn(gpus: int, argv: Sequence[str], script: str, rank0_extra_s: float = 0.0) -> str:
     """bench.py's entry decision.  Returns the plan for this process; for 'spawn' it runs the ranks and
-    exits with their status (the parent does no GPU work)."""
+    exits with their status (the parent does no GPU work).  rank0_extra_s: the work rank 0 does alone after the
+    other ranks return (bench.py's CPU baseline)."""
     p = plan(gpus, os.environ)
     if p == "spawn":
         print(f"[bench] WORLD_SIZE unset and --gpus {gpus}: starting {gpus} rank processes "
               f"(one per GPU, rendezvous on 127.0.0.1)", file=sys.stderr, flush=True)
-        raise SystemExit(spawn_ranks(gpus, [sys.executable, "-u", script, *argv]))
+        raise SystemExit(spawn_ranks(gpus, [sys.executable, "-u", script, *argv],
+                                     rank0_grace_s=300.0 + rank0_extra_s))
     return p

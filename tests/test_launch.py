@@ -151,3 +151,16 @@ def test_bench_records_the_loaded_library():
     assert rec["build"]["variant"] == "product" and rec["build"]["abi"] == "7"
     with pytest.raises(SystemExit):
         bench.lib_record(argparse.Namespace(variant="half"))     # the product build is not variant "half"
+
+
+def test_rank0_stuck_after_the_others_is_stopped():
+    """The other side of ADVICE r5: a rank 0 that hangs after every other rank exited cleanly is stopped after
+    rank0_grace_s (bench.py passes its CPU-baseline budget + 300 s), so a hung rank 0 cannot poll forever."""
+    import time
+    code = ("import os, time\n"
+            "time.sleep(3600 if os.environ['RANK'] == '0' else 0)\n")
+    t0 = time.time()
+    rc = launch.spawn_ranks(2, [sys.executable, "-c", code], env=_clean_env(), grace_s=1.0, straggler_s=1.0,
+                            rank0_grace_s=2.0)
+    assert rc == 124
+    assert time.time() - t0 < 30
