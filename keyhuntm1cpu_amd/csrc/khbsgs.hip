@@ -620,7 +620,7 @@ int khb_load_gate(khb_ctx* c, const uint8_t* gate, uint32_t log2_bits, uint32_t 
     KHB_TRY(c, hipMemcpy(c->d_gate1, f.data(), nb1 * 8, hipMemcpyHostToDevice));
     c->gate1_mask = (uint32_t)(nb1 - 1);
     // stage 0 (off by default, KHB_GATE0): KHB_GATE_STAGE0_AUTO puts a 2 MiB one-bit-per-member filter in front of a
-    // fold larger than 2 MiB (k >= 4, where the 16 MiB fold is read from the MALL for every x); none at k = 1, whose
+    // fold larger than 2 MiB (k >= 4, where the fold is read from the MALL for every x); none at k = 1, whose
     // 2 MiB fold is itself L2-resident.  With one probe every hi word is set (above), so the filter would pass
     // everything: none.
     const uint32_t z_log2 = c->gate0_log2 != KHB_GATE_STAGE0_AUTO ? c->gate0_log2 : f_log2 > 21 ? 21u : 0u;
