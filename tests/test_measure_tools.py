@@ -246,3 +246,17 @@ def test_power_handle_matches_full_pci_address():
     assert h is None and "3 amdsmi handles" in why
     FakeSmi.bdfs = {"h0": "0000:8b:00.0"}
     assert _handle_for_bdf(FakeSmi(), None) == ("h0", None)
+
+
+def test_energy_split_reproduces_design():
+    """tools/energy_split.py recomputes DESIGN.md §5's energy table from the committed evidence (r06c/d/f/g, r05c,
+    pmc_latest.json): VALU 12.6 nJ, non-VALU <= 0.13, zero-memory build 13.5, memory side in situ 4.85, product 18.35
+    nJ per giant step, and the product at 94.0 % of the compute-only ceiling."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "energy_split.py")], capture_output=True,
+                       text=True, check=True)
+    d = json.loads(r.stdout)
+    assert abs(d["valu_nj"] - 12.6) < 0.05 and d["non_valu_nj_total"] <= 0.13
+    assert abs(d["zero_memory"]["nj"] - 13.5) < 0.05 and abs(d["memory_side_in_situ_nj"] - 4.85) < 0.01
+    assert abs(d["product"]["nj"] - 18.35) < 0.01 and abs(d["product_over_compute_ceiling"] - 0.940) < 0.001
+    assert abs(d["compute_predicted_nj"] - d["zero_memory"]["nj"]) < 1.0      # within 1 nJ (VERDICT r5 item 5)
+    assert d["icache_miss_frac"] < 1e-4
