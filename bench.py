@@ -489,8 +489,11 @@ def main():
                              "gate skips for 99.96 % of x, plus the half prefix stream's 255 products per group",
                      "achieved": round(executed, 3), "frac": round(executed / PEAK_MULOPS_T, 4),
                      "frac_at_2p16ghz": round(executed / PEAK_MULOPS_T_2P16, 4)}
-    pmc_path = os.path.join(REPO, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc_path):
+    # the PMC record of this run's k: profiles/pmc_latest.json (k = 1, configs B and D) or pmc_latest_k4.json (C)
+    pmc_path = os.path.join(REPO, "profiles", "pmc_latest.json" if args.k == 1 else "pmc_latest_k%d.json" % args.k)
+    if not os.path.exists(pmc_path):
+        roofline["traffic_note"] = "no PMC record for k = %d (%s)" % (args.k, os.path.relpath(pmc_path, REPO))
+    else:
         try:
             with open(pmc_path) as f:
                 pmc = json.load(f)

@@ -9,7 +9,8 @@
 #   3. config E: bench.py --workload address, and SQ_INSTS_VALU of one 8-chunk launch of the product
 #      library and of the hash-less addrwalk build (the x/y walk term of the floor, tools/addr_floor.py).
 # Usage: bash tools/gpu/round_profile.sh <tag> [steps]     Env: PARTS (default "trace pmc address"), PMC_JOBS
-# (chunks per PMC launch, default 4096 = the bench's auto batch at 4 waves/SIMD).
+# (chunks per PMC launch, default 4096 = the bench's auto batch at 4 waves/SIMD), K (default 1; K=4 PMC_JOBS=16384
+# PARTS=pmc gives config C's record, profiles/pmc_latest_k4.json).
 set -o pipefail
 export TMPDIR=/tmp
 TAG=${1:-prof}
@@ -19,6 +20,7 @@ mkdir -p $O
 L=keyhuntm1cpu_amd/lib/libkhbsgs.so
 W=keyhuntm1cpu_amd/lib/variants/libkhbsgs_addrwalk.so
 J=${PMC_JOBS:-4096}
+export K=${K:-1}          # the geometry's k (perf_variants reads K; K=4 with PMC_JOBS=16384 is config C's launch)
 PARTS=${PARTS:-trace pmc address}
 step() { echo "[$(date +%T)] $*"; }
 has() { case " $PARTS " in *" $1 "*) return 0;; esac; return 1; }
@@ -47,7 +49,7 @@ for d in $O/pmc_fetch_0 $O/pmc_fetch_13 $O/pmc_write_0 $O/pmc_sq $O/pmc_sq2; do 
   f=$(find $d -name "*counter_collection.csv" | sort | tail -1)
   [ "$f" = "$d/pmc_counter_collection.csv" ] || cp "$f" $d/pmc_counter_collection.csv
 done
-python3 tools/pmc_summary.py $O $J $O/pmc_latest.json > /dev/null || exit 1
+python3 tools/pmc_summary.py $O $J $O/pmc_latest.json $K > /dev/null || exit 1
 fi
 
 if has address; then

@@ -28,7 +28,8 @@ itself: lanes = its grid size, waves per SIMD = lanes / (256 CUs x 4 SIMDs x 64)
 mode (k_giant_scan<7|8|9> are the gated scans), and the build (half prefix stream, groups per item, variant) from the
 profiled library's khb_build_info (KHB_PMC_LIB, default the in-tree libkhbsgs.so).  A dispatch without those columns
 is an error, not a default.
-Usage: python tools/pmc_summary.py <dir with the pmc_* subdirs> <chunks per launch> [out.json] [k]"""
+Usage: python tools/pmc_summary.py <dir with the pmc_* subdirs> <chunks per launch> [out.json] [k]
+(k = 4: profiles/pmc_latest_k4.json, the record bench.py attaches to --k 4 lines)"""
 import collections
 import csv
 import json
@@ -39,6 +40,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 GROUPS = 4096          # k=1 default geometry: groups per chunk (cycles)
+GROUPS_BY_K = {1: 4096, 4: 1024}   # cycles per chunk of the default -n 2^44 geometry
 CUS, SIMDS = 256, 4
 GATED_MODES = (7, 8, 9)   # scan_kernels.hpp kScanG, kScanG1, kScanG2
 
@@ -74,7 +76,7 @@ def main():
     src, chunks = sys.argv[1], int(sys.argv[2])
     dst = sys.argv[3] if len(sys.argv) > 3 else os.path.join(REPO, "profiles", "pmc_latest.json")
     kk = int(sys.argv[4]) if len(sys.argv) > 4 else 1
-    steps = chunks * GROUPS * 1024
+    steps = chunks * GROUPS_BY_K[kk] * 1024
     real_all, real_meta = dispatches(os.path.join(src, "pmc_fetch_0"), meta=True)
     real_f = real_all[-1]
     cfg = kernel_config(real_meta[-1])
