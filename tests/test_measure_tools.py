@@ -13,6 +13,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tools"))
 
@@ -117,14 +119,16 @@ def test_pmc_summary_refuses_a_dispatch_without_its_configuration(tmp_path):
     assert r.returncode != 0 and "grid size" in (r.stderr + r.stdout)
 
 
-def test_committed_pmc_latest_reproduces_from_its_csvs(tmp_path):
-    """profiles/pmc_latest.json (bench.py's roofline.traffic) equals a rerun of the summary on the raw
-    CSVs it names."""
-    with open(os.path.join(REPO, "profiles", "pmc_latest.json")) as f:
+@pytest.mark.parametrize("name", ["pmc_latest.json", "pmc_latest_k4.json"])
+def test_committed_pmc_latest_reproduces_from_its_csvs(tmp_path, name):
+    """profiles/pmc_latest.json (bench.py's roofline.traffic for k = 1) and pmc_latest_k4.json (for --k 4) equal a
+    rerun of the summary on the raw CSVs they name."""
+    with open(os.path.join(REPO, "profiles", name)) as f:
         cur = json.load(f)
     out = tmp_path / "again.json"
     subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"), os.path.join(REPO, cur["source"]),
-                    str(cur["chunks_per_launch"]), str(out)], capture_output=True, text=True, check=True)
+                    str(cur["chunks_per_launch"]), str(out), str(cur["k"])], capture_output=True, text=True,
+                   check=True)
     again = json.loads(out.read_text())
     for k in ("hbm_bytes_per_launch", "bytes_per_giant_step", "gate_read_requests_per_giant_step",
               "valu_instr_per_giant_step", "valu_util_pct", "valu_dual_issue_frac", "level0_gate", "lanes",
