@@ -47,7 +47,8 @@ extern "C" {
  * them changes.  A binding checks khb_abi_version() == the KHB_ABI_VERSION it was written for before
  * any other call (khb_stats gained launch_begin_ms/launch_end_ms/shader_mhz in ABI 3 and 4; ABI 5 added
  * khb_load_check_tables / khb_check; ABI 6 added khb_stats.event_ms; ABI 7 added khb_build_info,
- * khb_set_gate_stage0, KHB_EHANDOFF / khb_last_handoff and the -m address endomorphism). */
+ * khb_set_gate_stage0 / khb_gate_stages, KHB_EHANDOFF / khb_last_handoff and the -m address endomorphism
+ * (KHB_SEARCH_ENDOMORPHISM, khb_addr_hit.kind = form | e << 2)). */
 #define KHB_ABI_VERSION 7
 int khb_abi_version(void);
 /* What this library was built as, one line of `key=value` words: abi, arch, variant ("product" for the in-tree
