@@ -347,3 +347,36 @@ def test_cli_endomorphism_lambda_multiples(tmp_path, keys, ora):
     totals = [int(m) for m in re.findall(r"Total (\d+) keys in", r.stdout)]
     assert totals, r.stdout[-2000:]
     assert all(t % (6 * n_seq) == 0 and t // 6 <= (1 << 33) for t in totals)
+
+
+@pytest.mark.parametrize("stride,endo", [(3, False), (0x100000001, True)])
+def test_addr_stride_hits_match_oracle(eng, ora, stride, endo):
+    """-I stride (keyhunt.cpp:790-797, init_generator 4386-4399: Gn[i] = (i+1)*stride*G), with and without -e: the GPU's
+    bloom-hit set over 16 groups equals the oracle's group loop at the same stride, and the host confirmation of every
+    hit (khh_addr_confirm: key = base + (1024 g + t) * stride, then lambda^e) recovers exactly the oracle's keys, which
+    are the planted ones."""
+    from tests.helpers import endo_planted_text
+    rng = random.Random(stride)
+    base, ngroups = 0x5000000000 + 7, 16
+    picks = [base + stride * t for t in rng.sample(range(1024 * ngroups), 400)]
+    if endo:
+        text, planted = endo_planted_text(ora, picks, 90)
+    else:
+        text = "\n".join(ora.pub_hash160(ora.pubkey(k), i % 2 == 0).hex() for i, k in enumerate(picks)) + "\n"
+        planted = [(k, i % 2 == 0, 0) for i, k in enumerate(picks)]
+    search = 2 | (ora.SEARCH_ENDO if endo else 0)
+    A = khhost.Addr(text, n_seq=1024 * ngroups, stride=stride, gpl=4)
+    _load(eng, A)
+    O = ora.AddrTable(text)
+    gen = ora.AddrGen(stride)
+    hits, keys = [], []
+    for g in range(ngroups):
+        h, k, _ = gen.group(O, base + 1024 * stride * g, search)
+        hits += [(g, t, kind) for t, kind in h]
+        keys += k
+    got, st = eng.addr_scan(khhost.pubkey(base + 512 * stride), 0, ngroups, search)
+    assert st.giant_steps == 1024 * ngroups
+    assert sorted((g, t, kind) for _, g, t, kind in got) == sorted(hits)
+    assert sorted(keys) == sorted(K for K, _, _ in planted)
+    conf = [A.confirm(base + stride * (1024 * g + t), kind) for _, g, t, kind in got]
+    assert sorted(r[0] for r in conf if r) == sorted(keys)
