@@ -380,3 +380,27 @@ def test_addr_stride_hits_match_oracle(eng, ora, stride, endo):
     assert sorted(keys) == sorted(K for K, _, _ in planted)
     conf = [A.confirm(base + stride * (1024 * g + t), kind) for _, g, t, kind in got]
     assert sorted(r[0] for r in conf if r) == sorted(keys)
+
+
+def test_cli_rmd160_endomorphism_uncompressed(tmp_path, keys, ora):
+    """keyhunt_amd -m rmd160 -e -l uncompress: a hash160 file holding the uncompressed hash160s of lambda^2 * k20 and of
+    n - lambda * k21 (the negated point (beta*x, p - y), kind 3 | 1 << 2) is solved over [1, 2^33): each key is reported
+    once with its uncompressed pubkey (keyhunt.cpp:2800-2920 -e uncompressed paths), and the totals count x6 keys."""
+    import re
+    k20, k21 = int(keys["20"]["key"], 16), int(keys["21"]["key"], 16)
+    lam, lam2 = ora.endo_constants(0)[0], ora.endo_constants(1)[0]
+    K1 = lam2 * k20 % N
+    K2 = N - lam * k21 % N
+    text = "\n".join(khhost.hash160(khhost.pubkey(K), False).hex() for K in (K1, K2)) + "\n"
+    (tmp_path / "endo.rmd").write_text(text)
+    n_seq = 1 << 28
+    r = _cli(["-m", "rmd160", "-f", "endo.rmd", "-e", "-l", "uncompress", "-r", "1:200000000", "-n", hex(n_seq),
+              "-q", "-s", "1"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "[+] Endomorphism enabled\n" in r.stdout
+    for K in (K1, K2):
+        assert r.stdout.count(f"Hit! Private Key: {K:x}\n") == 1, K
+        xy = khhost.pubkey(K)
+        assert f"pubkey: 04{xy.hex()}\n" in r.stdout, K
+    totals = [int(m) for m in re.findall(r"Total (\d+) keys in", r.stdout)]
+    assert totals and all(t % (6 * n_seq) == 0 for t in totals)
